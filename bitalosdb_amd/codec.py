@@ -1,0 +1,200 @@
+"""Host-side mirror of the reference's bithash record-codec surface, backed by
+the gfx950 kernels through the C-ABI (include/bithashgpu.h).
+
+Reference surface this mirrors (zuoyebang/bitalosdb v2):
+  * compress.Compressor: NoCompressor / SnappyCompressor     internal/compress/compress.go:26-89
+  * block2Reader.readRecord -> (*InternalKey, value, FileNum)  bithash/block2.go:57-66
+  * Reader.readData errors                                     bithash/reader.go:233-272, error.go
+  * Writer.Add / BithashWriter.Add + maybeSplitTable           bithash/writer.go:230-283, bithash_writer.go:25-67
+  * hash.Fnv32, crc.New(b).Value()                             internal/hash/fnv.go:19-23, internal/crc/crc.go
+  * TableIterator / Writer.rebuild scans                       bithash/table.go:358-395, writer.go:539-583
+
+torch is used only as device-memory plumbing (tensors hold the buffers; their
+data_ptr()s cross the C-ABI).  Every computation happens in the HIP library.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib as B
+from ._lib import CODEC_NONE, CODEC_SNAPPY, DESC_DT, HANDLE_DT  # noqa: F401
+
+# compress.CompressTypeNo / CompressTypeSnappy (compress.go:21-24)
+NoCompressor = CODEC_NONE
+SnappyCompressor = CODEC_SNAPPY
+
+# Go sentinel errors each per-block status maps onto (bithash/error.go, golang/snappy)
+STATUS_ERRORS = {
+    B.ST_RECORD_NIL: "bithash: read record nil",                 # ErrBhReadRecordNil
+    B.ST_ILLEGAL_LENGTH: "bithash: illegal block length",        # ErrBhIllegalBlockLength
+    B.ST_INCOMPLETE: "bithash: readAt incomplete",               # ErrBhReadAtIncomplete / io.EOF
+    B.ST_SNAPPY_CORRUPT: "snappy: corrupt input",                # snappy.ErrCorrupt
+    B.ST_SNAPPY_TOO_LARGE: "snappy: decoded block is too large",
+    B.ST_CRC_MISMATCH: "bithash: record crc mismatch",
+    B.ST_KEY_TOO_LARGE: "bithash: key too large",                # ErrBhKeyTooLarge
+    B.ST_VALUE_TOO_LARGE: "bithash: value too large",            # ErrBhValueTooLarge
+    B.ST_DATA_MAX_EXCEEDED: "bithash: panic add exceed data max size",
+}
+
+
+class BithashCodecError(Exception):
+    def __init__(self, status):
+        super().__init__(STATUS_ERRORS.get(int(status), "status %d" % int(status)))
+        self.status = int(status)
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr() if t.numel() else None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data if t.size else None
+    return int(t)
+
+
+def as_device_bytes(x, device):
+    """numpy/bytes -> uint8 CUDA tensor (plumbing)."""
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.uint8) if x.device != device else x.view(torch.uint8)
+    a = np.frombuffer(bytes(x), dtype=np.uint8) if isinstance(x, (bytes, bytearray)) else np.ascontiguousarray(x).view(np.uint8).reshape(-1)
+    return torch.from_numpy(a.copy()).to(device)
+
+
+def handles_tensor(handles, device):
+    a = np.ascontiguousarray(handles, dtype=HANDLE_DT)
+    return torch.from_numpy(a.view(np.uint8).copy()).to(device)
+
+
+def desc_numpy(desc_t):
+    return desc_t.cpu().numpy().view(DESC_DT).reshape(-1)
+
+
+@dataclass
+class DecodedBatch:
+    desc: torch.Tensor          # uint8 [n*40] device: bhg_desc[n]
+    vals: torch.Tensor          # uint8 device (snappy) or None
+    val_off: torch.Tensor       # uint8 view of u64[n+1] (snappy) or None
+
+    def desc_np(self):
+        return desc_numpy(self.desc)
+
+    def val_off_np(self):
+        return None if self.val_off is None else self.val_off.cpu().numpy().view(np.uint64)
+
+
+class BithashCodec:
+    """One bhg_ctx on one GPU (the cgo shim's Go-side object, in Python)."""
+
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise B.BhgError("no GPU visible: the bithash codec has no CPU path")
+        self.device = torch.device("cuda", device)
+        self.L = B.lib()
+        self.ctx = self.L.bhg_create(device, 0)
+        if not self.ctx:
+            raise B.BhgError("bhg_create(%d) failed" % device)
+
+    def close(self):
+        if self.ctx:
+            self.L.bhg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def sync(self):
+        torch.cuda.current_stream(self.device).synchronize()
+
+    # ---- decode ----
+    def decode_batch(self, src, src_len, handles, n, compressor=NoCompressor, expected_crc=None,
+                     out_desc=None, out_vals=None, out_val_off=None, stream=None):
+        """Device-resident batch decode (bhg_decode_batch).  src/handles/... are
+        CUDA tensors (or raw device pointers as ints)."""
+        dev = self.device
+        if out_desc is None:
+            out_desc = torch.empty(n * DESC_DT.itemsize, dtype=torch.uint8, device=dev)
+        cap = 0
+        if compressor == SnappyCompressor:
+            if out_val_off is None:
+                out_val_off = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev)
+            if out_vals is not None:
+                cap = out_vals.numel() if isinstance(out_vals, torch.Tensor) else int(out_vals[1])
+                out_vals = out_vals if isinstance(out_vals, torch.Tensor) else out_vals[0]
+        rc = self.L.bhg_decode_batch(self.ctx, _ptr(src), src_len, _ptr(handles), n, compressor,
+                                     _ptr(expected_crc), _ptr(out_desc), _ptr(out_vals), cap, _ptr(out_val_off),
+                                     stream if stream is not None else self._stream())
+        B.check(self.ctx, rc, "bhg_decode_batch")
+        return DecodedBatch(out_desc, out_vals, out_val_off)
+
+    def decode(self, src, handles, compressor=NoCompressor, expected_crc=None):
+        """Convenience: host arrays in, device decode, results as numpy.
+        Snappy runs two passes: sizes -> allocate -> decode (the library fills val_off)."""
+        dev = self.device
+        src_t = as_device_bytes(src, dev)
+        h_t = handles_tensor(handles, dev)
+        n = len(handles)
+        exp_t = None
+        if expected_crc is not None:
+            exp_t = torch.from_numpy(np.ascontiguousarray(expected_crc, dtype=np.uint32).view(np.int32).copy()).to(dev)
+        if compressor == SnappyCompressor:
+            probe = self.decode_batch(src_t, src_t.numel(), h_t, n, compressor, exp_t)
+            self.sync()
+            total = int(probe.val_off_np()[-1]) if n else 0
+            vals = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+            res = self.decode_batch(src_t, src_t.numel(), h_t, n, compressor, exp_t, out_vals=vals)
+            self.sync()
+            return res.desc_np(), vals.cpu().numpy()[:total], res.val_off_np()
+        res = self.decode_batch(src_t, src_t.numel(), h_t, n, compressor, exp_t)
+        self.sync()
+        return res.desc_np(), None, None
+
+    def decode_host(self, src, handles, compressor=NoCompressor, expected_crc=None, out_vals_cap=None):
+        """End-to-end path: host buffers in and out (bhg_decode_batch_host)."""
+        src = np.ascontiguousarray(np.frombuffer(src, np.uint8) if isinstance(src, (bytes, bytearray)) else src,
+                                   dtype=np.uint8)
+        h = np.ascontiguousarray(handles, dtype=HANDLE_DT)
+        n = len(h)
+        desc = np.zeros(n, dtype=DESC_DT)
+        exp = None if expected_crc is None else np.ascontiguousarray(expected_crc, dtype=np.uint32)
+        off = np.zeros(n + 1, dtype=np.uint64) if compressor == SnappyCompressor else None
+        cap = 0
+        vals = None
+        if compressor == SnappyCompressor:
+            cap = out_vals_cap if out_vals_cap is not None else max(1, int(src.size) * 22)
+            vals = np.zeros(max(cap, 1), dtype=np.uint8)
+        rc = self.L.bhg_decode_batch_host(self.ctx, _ptr(src), src.size, _ptr(h), n, compressor, _ptr(exp),
+                                          _ptr(desc), _ptr(vals), cap, _ptr(off))
+        B.check(self.ctx, rc, "bhg_decode_batch_host")
+        return desc, (None if vals is None else vals[:int(off[-1])]), off
+
+    # ---- primitives ----
+    def crc_batch(self, src_t, handles_t, n):
+        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        rc = self.L.bhg_crc32c_masked_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(out),
+                                            self._stream())
+        B.check(self.ctx, rc, "bhg_crc32c_masked_batch")
+        return out
+
+    def fnv_batch(self, src_t, handles_t, n):
+        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        rc = self.L.bhg_fnv32_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(out),
+                                    self._stream())
+        B.check(self.ctx, rc, "bhg_fnv32_batch")
+        return out
+
+
+def read_record_status(desc_row):
+    """block2Reader.readRecord (block2.go:57-66) outcome for one descriptor:
+    raises the Go sentinel the reader would return, else (key_off, key_len, val_off, val_len)."""
+    if int(desc_row["status"]) != B.ST_OK:
+        raise BithashCodecError(desc_row["status"])
+    return (int(desc_row["key_off"]), int(desc_row["key_len"]), int(desc_row["val_off"]), int(desc_row["val_len"]))

@@ -1,0 +1,282 @@
+// bhg_api.hip -- implementation of the C-ABI in include/bithashgpu.h.
+//
+// Host orchestration only: argument checks, per-context scratch, launch
+// sequencing on the caller's stream.  All byte work runs in the kernels
+// (bhg_decode.hip, bhg_encode.hip, bhg_scan.hip); there is no CPU fallback:
+// without a usable HIP device bhg_create() fails and every entry point
+// returns an error.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "bhg_internal.h"
+
+struct bhg_ctx {
+    int device;
+    hipStream_t stream;
+    int num_cus;
+    int lane_wgs_per_cu;
+    char err[512];
+    std::mutex mu;          // guards scratch growth and the host-path buffers
+    void *scratch = nullptr;
+    size_t scratch_cap = 0;
+    // host (end-to-end) path device buffers
+    void *h_src = nullptr; size_t h_src_cap = 0;
+    void *h_aux = nullptr; size_t h_aux_cap = 0;
+};
+
+namespace {
+
+void set_err(bhg_ctx *c, const char *fmt, ...) {
+    if (!c) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(c->err, sizeof c->err, fmt, ap);
+    va_end(ap);
+}
+
+int hip_fail(bhg_ctx *c, hipError_t e, const char *what) {
+    set_err(c, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? BHG_ENOMEM : BHG_EHIP;
+}
+
+#define HIP_TRY(ctx, expr)                                     \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+bhg::Launch launch_of(bhg_ctx *c, void *stream) {
+    bhg::Launch L;
+    L.stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    L.num_cus = c->num_cus;
+    L.lane_wgs_per_cu = c->lane_wgs_per_cu;
+    return L;
+}
+
+// grow ctx scratch (synchronous; never inside a captured region)
+int ensure_buf(bhg_ctx *c, void **buf, size_t *cap, size_t need) {
+    if (need <= *cap) return BHG_OK;
+    if (*buf) {
+        hipStreamSynchronize(c->stream);
+        hipDeviceSynchronize();
+        hipFree(*buf);
+        *buf = nullptr;
+        *cap = 0;
+    }
+    size_t sz = need + need / 4 + 4096;
+    hipError_t e = hipMalloc(buf, sz);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(scratch)");
+    *cap = sz;
+    return BHG_OK;
+}
+
+int set_device(bhg_ctx *c) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return hip_fail(c, e, "hipSetDevice");
+    return BHG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bhg_abi_version(void) { return BHG_ABI_VERSION; }
+
+int bhg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+bhg_ctx *bhg_create(int device, int flags) {
+    (void)flags;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return nullptr;
+    bhg_ctx *c = new bhg_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->lane_wgs_per_cu = 4;
+    if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
+    c->err[0] = 0;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void bhg_destroy(bhg_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    if (c->scratch) hipFree(c->scratch);
+    if (c->h_src) hipFree(c->h_src);
+    if (c->h_aux) hipFree(c->h_aux);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *bhg_last_error(const bhg_ctx *c) { return c ? c->err : "null context"; }
+
+void *bhg_stream(bhg_ctx *c) { return c ? reinterpret_cast<void *>(c->stream) : nullptr; }
+
+int bhg_stream_sync(bhg_ctx *c, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, hipStreamSynchronize(stream ? reinterpret_cast<hipStream_t>(stream) : c->stream));
+    return BHG_OK;
+}
+
+void *bhg_malloc_device(bhg_ctx *c, uint64_t bytes) {
+    if (!c || set_device(c)) return nullptr;
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e != hipSuccess) { hip_fail(c, e, "hipMalloc"); return nullptr; }
+    return p;
+}
+
+int bhg_free_device(bhg_ctx *c, void *p) {
+    if (!c) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, hipFree(p));
+    return BHG_OK;
+}
+
+void *bhg_malloc_host(bhg_ctx *c, uint64_t bytes) {
+    if (!c || set_device(c)) return nullptr;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) { hip_fail(c, e, "hipHostMalloc"); return nullptr; }
+    return p;
+}
+
+int bhg_free_host(bhg_ctx *c, void *p) {
+    if (!c) return BHG_EINVAL;
+    HIP_TRY(c, hipHostFree(p));
+    return BHG_OK;
+}
+
+int bhg_memcpy_h2d(bhg_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!c || (!dst && bytes) || (!src && bytes)) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, L.stream));
+    return BHG_OK;
+}
+
+int bhg_memcpy_d2h(bhg_ctx *c, void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!c || (!dst && bytes) || (!src && bytes)) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, L.stream));
+    return BHG_OK;
+}
+
+int bhg_memset_device(bhg_ctx *c, void *dst, int value, uint64_t bytes, void *stream) {
+    if (!c || (!dst && bytes)) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    HIP_TRY(c, hipMemsetAsync(dst, value, bytes, L.stream));
+    return BHG_OK;
+}
+
+int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                     int codec, const uint32_t *expected_crc, bhg_desc *out_desc, uint8_t *out_vals,
+                     uint64_t out_vals_cap, uint64_t *out_val_off, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (codec != BHG_CODEC_NONE && codec != BHG_CODEC_SNAPPY) { set_err(c, "bad codec %d", codec); return BHG_EINVAL; }
+    if (n == 0) {
+        if (codec == BHG_CODEC_SNAPPY && out_val_off) return bhg_memset_device(c, out_val_off, 0, 8, stream);
+        return BHG_OK;
+    }
+    if (!handles || !out_desc || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    HIP_TRY(c, bhg::launch_decode_lane(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
+    if (codec == BHG_CODEC_SNAPPY) {
+        {
+            std::lock_guard<std::mutex> g(c->mu);
+            if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(n))) return r;
+        }
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, c->scratch));
+        HIP_TRY(c, bhg::launch_snappy_wave(L, src, src_len, handles, n, out_desc, out_vals, out_vals ? out_vals_cap : 0,
+                                           out_val_off));
+    }
+    return BHG_OK;
+}
+
+int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                          int codec, const uint32_t *expected_crc, bhg_desc *out_desc, uint8_t *out_vals,
+                          uint64_t out_vals_cap, uint64_t *out_val_off) {
+    if (!c) return BHG_EINVAL;
+    if (n == 0) {
+        if (codec == BHG_CODEC_SNAPPY && out_val_off) out_val_off[0] = 0;
+        return BHG_OK;
+    }
+    if (!handles || !out_desc || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    const size_t hb = (size_t)n * sizeof(bhg_handle), db = (size_t)n * sizeof(bhg_desc);
+    const size_t eb = expected_crc ? (size_t)n * 4 : 0, ob = codec == BHG_CODEC_SNAPPY ? ((size_t)n + 1) * 8 : 0;
+    const size_t vb = codec == BHG_CODEC_SNAPPY ? (size_t)out_vals_cap : 0;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    if (int r = ensure_buf(c, &c->h_src, &c->h_src_cap, src_len + 64)) return r;
+    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(vb) + 256)) return r;
+    uint8_t *a = reinterpret_cast<uint8_t *>(c->h_aux);
+    bhg_handle *dh = reinterpret_cast<bhg_handle *>(a); a += al(hb);
+    bhg_desc *dd = reinterpret_cast<bhg_desc *>(a); a += al(db);
+    uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(eb);
+    uint64_t *doff = ob ? reinterpret_cast<uint64_t *>(a) : nullptr; a += al(ob);
+    uint8_t *dv = vb ? a : nullptr;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(c->h_src, src, src_len, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(dh, handles, hb, hipMemcpyHostToDevice, s));
+    if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc, eb, hipMemcpyHostToDevice, s));
+    bhg::Launch L = launch_of(c, nullptr);
+    HIP_TRY(c, bhg::launch_decode_lane(L, reinterpret_cast<const uint8_t *>(c->h_src), src_len, dh, n, codec, de, dd, doff));
+    if (codec == BHG_CODEC_SNAPPY) {
+        if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(n))) return r;
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, doff, doff, n, c->scratch));
+        HIP_TRY(c, bhg::launch_snappy_wave(L, reinterpret_cast<const uint8_t *>(c->h_src), src_len, dh, n, dd, dv,
+                                           dv ? out_vals_cap : 0, doff));
+        HIP_TRY(c, hipMemcpyAsync(out_val_off, doff, ob, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+        uint64_t total = out_val_off[n];
+        if (total > out_vals_cap) total = out_vals_cap;
+        if (total && out_vals) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(out_desc, dd, db, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    return BHG_OK;
+}
+
+int bhg_crc32c_masked_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                            uint32_t *out_crc, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (n == 0) return BHG_OK;
+    if (!handles || !out_crc || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, bhg::launch_crc_ranges(launch_of(c, stream), src, src_len, handles, n, out_crc));
+    return BHG_OK;
+}
+
+int bhg_fnv32_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                    uint32_t *out_fnv, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (n == 0) return BHG_OK;
+    if (!handles || !out_fnv || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, bhg::launch_fnv_ranges(launch_of(c, stream), src, src_len, handles, n, out_fnv));
+    return BHG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// bhg_internal.h -- host-side glue shared by the kernel translation units
+// and the C-ABI implementation (bhg_api.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bithashgpu.h"
+
+namespace bhg {
+
+struct Launch {
+    hipStream_t stream;
+    int num_cus;        // 256 on MI355X
+    int lane_wgs_per_cu;  // persistent workgroups per CU for the lane-per-block kernels
+};
+
+// persistent grid for lane-per-block kernels: enough workgroups to fill the
+// chip (LDS-limited residency), never more than the work needs
+inline uint32_t lane_grid(const Launch &L, uint64_t n, uint32_t block) {
+    uint64_t need = (n + block - 1) / block;
+    uint64_t cap = (uint64_t)L.num_cus * (uint64_t)(L.lane_wgs_per_cu > 0 ? L.lane_wgs_per_cu : 4);
+    uint64_t g = need < cap ? need : cap;
+    return g == 0 ? 1u : (uint32_t)g;
+}
+
+// bhg_decode.hip
+hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                              int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                              bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
+hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                             uint32_t *out);
+hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                             uint32_t *out);
+
+// bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
+// scratch must hold scan_scratch_bytes(n).
+size_t scan_scratch_bytes(uint64_t n);
+hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch);
+
+}  // namespace bhg

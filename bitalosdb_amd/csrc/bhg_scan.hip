@@ -1,0 +1,110 @@
+// bhg_scan.hip -- exclusive prefix sum over u64 (decoded-size -> output
+// offsets for snappy values, record lengths -> record positions for encode).
+// Reduce-then-scan: per-workgroup chunk sums, a recursive scan of the sums,
+// then a chunk-local scan plus base.  Each workgroup covers 2048 elements
+// (256 threads x 8), so 1M sizes need 489 workgroups and one recursion level.
+#include "bhg_internal.h"
+
+namespace bhg {
+
+#define SCAN_T 256
+#define SCAN_PER 8
+#define SCAN_CHUNK (SCAN_T * SCAN_PER)
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one value per thread; returns exclusive prefix, *total = sum
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total) {
+    __shared__ uint64_t wsum[SCAN_T / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_T / 64; k++) {
+        if (k < w) before += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return before + inc - v;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_chunk_sums(const uint64_t *__restrict__ in, uint64_t n,
+                                                       uint64_t *__restrict__ sums) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        uint64_t idx = b0 + (uint64_t)threadIdx.x * SCAN_PER + k;
+        if (idx < n) s += in[idx];
+    }
+    uint64_t tot;
+    block_excl_scan(s, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// chunk-local exclusive scan + base (base = bases[blockIdx.x] or 0); in may alias out
+__global__ __launch_bounds__(SCAN_T) void k_chunk_scan(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                       const uint64_t *__restrict__ bases, int write_total) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint64_t v[SCAN_PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        uint64_t idx = b0 + (uint64_t)threadIdx.x * SCAN_PER + k;
+        v[k] = idx < n ? in[idx] : 0;
+        s += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(s, &tot) + (bases ? bases[blockIdx.x] : 0);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        uint64_t idx = b0 + (uint64_t)threadIdx.x * SCAN_PER + k;
+        if (idx < n) out[idx] = run;
+        run += v[k];
+    }
+    if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_T - 1) out[n] = run;
+}
+
+size_t scan_scratch_bytes(uint64_t n) {
+    size_t bytes = 0;
+    while (n > SCAN_CHUNK) {
+        n = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+        bytes += (n + 1) * sizeof(uint64_t);
+    }
+    return bytes + 64;
+}
+
+// exclusive scan of in[0..n) into out[0..n], out[n] = total.  in may equal out.
+hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch) {
+    if (n == 0) {
+        return hipMemsetAsync(out, 0, sizeof(uint64_t), L.stream);
+    }
+    const uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    if (nb == 1) {
+        hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(SCAN_T), 0, L.stream, in, out, n, (const uint64_t *)nullptr, 1);
+        return hipGetLastError();
+    }
+    uint64_t *sums = reinterpret_cast<uint64_t *>(scratch);
+    uint8_t *rest = reinterpret_cast<uint8_t *>(scratch) + (nb + 1) * sizeof(uint64_t);
+    hipLaunchKernelGGL(k_chunk_sums, dim3((uint32_t)nb), dim3(SCAN_T), 0, L.stream, in, n, sums);
+    hipError_t e = launch_exclusive_scan_u64(L, sums, sums, nb, rest);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_chunk_scan, dim3((uint32_t)nb), dim3(SCAN_T), 0, L.stream, in, out, n, (const uint64_t *)sums, 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // total = sums[nb]
+    return hipMemcpyAsync(out + n, sums + nb, sizeof(uint64_t), hipMemcpyDeviceToDevice, L.stream);
+}
+
+}  // namespace bhg

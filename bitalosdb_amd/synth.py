@@ -1,0 +1,91 @@
+"""Synthetic bithash workloads built directly in HBM.
+
+The reference's tests draw keys/values from utils.FuncRandBytes' alphabet
+(internal/utils/func.go:22-30) with an unseeded math/rand; here a seeded
+torch generator stands in, so inputs are reproducible.  Records are laid out
+exactly as Writer.add writes them (block2.go:73-105): tables of
+TableMaxSize=128 MiB split after the add that crosses the limit
+(bithash_writer.go:47-67), each data region followed by the 12-byte zero
+terminator (writer.go:393-407).  The per-table tail (conflict / indexhash /
+meta / footer) is not materialised: the decode path never reads it.
+"""
+import numpy as np
+import torch
+
+ALPHABET = b"1qaz2wsx3edc4rfv5tgb6yhn7ujm8ik9ol0pabcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"
+TABLE_MAX = 128 << 20
+SEED = 0xB17A105DB
+
+
+def records_per_table(rec_len, table_max=TABLE_MAX):
+    return -(-table_max // rec_len)      # the add that reaches >= table_max stays in the table
+
+
+def _alpha(device):
+    return torch.tensor(list(ALPHABET), dtype=torch.uint8, device=device)
+
+
+def _rand_alpha(g, shape, device, alpha):
+    idx = torch.randint(0, len(ALPHABET), shape, generator=g, device=device, dtype=torch.int64)
+    return alpha[idx]
+
+
+def uniform_tables(n, key_len=32, val_len=1024, device="cuda", seed=SEED, table_max=TABLE_MAX, first_file_num=1,
+                   chunk=1 << 16):
+    """n records of (key_len, val_len) packed into 128 MiB tables on `device`.
+
+    Returns (src uint8 tensor, handles numpy HANDLE_DT, meta dict)."""
+    from ._lib import HANDLE_DT
+    device = torch.device(device)
+    klen = key_len + 8
+    L = 12 + klen + val_len
+    R = records_per_table(L, table_max)
+    ntab = -(-n // R)
+    tbytes = R * L + 12
+    total = (ntab - 1) * tbytes + (n - (ntab - 1) * R) * L + 12
+    src = torch.zeros(total, dtype=torch.uint8, device=device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    alpha = _alpha(device)
+    hdr = np.zeros(12, dtype=np.uint8)
+    for t in range(ntab):
+        r0, r1 = t * R, min(n, (t + 1) * R)
+        view = src[t * tbytes:t * tbytes + (r1 - r0) * L].view(r1 - r0, L)
+        hdr[:] = np.frombuffer(np.array([klen, val_len, first_file_num + t], dtype="<u4").tobytes(), dtype=np.uint8)
+        view[:, :12] = torch.from_numpy(hdr.copy()).to(device)
+        for c0 in range(0, r1 - r0, chunk):
+            c1 = min(r1 - r0, c0 + chunk)
+            m = c1 - c0
+            view[c0:c1, 12:12 + key_len] = _rand_alpha(g, (m, key_len), device, alpha)
+            seq = torch.arange(r0 + c0 + 1, r0 + c1 + 1, device=device, dtype=torch.int64)
+            tr = (seq << 8) | 1
+            view[c0:c1, 12 + key_len:12 + klen] = tr.view(torch.uint8).view(m, 8)
+            view[c0:c1, 12 + klen:] = _rand_alpha(g, (m, val_len), device, alpha)
+    h = np.zeros(n, dtype=HANDLE_DT)
+    i = np.arange(n, dtype=np.uint64)
+    h["offset"] = (i // R) * np.uint64(tbytes) + (i % R) * np.uint64(L)
+    h["length"] = L
+    meta = dict(n=n, rec_len=L, records_per_table=R, tables=ntab, table_bytes=tbytes, src_bytes=total,
+                block_bytes=n * L)
+    return src, h, meta
+
+
+def compressible_values(rng, n_vals, val_len, dict_size=4096, fresh=0.2):
+    """Values of tokens (4-64 B) drawn from a seeded dictionary, ~20 % fresh
+    random bytes -- the SURVEY §8d C3 generator (numpy, host)."""
+    d = rng.integers(0, 256, size=dict_size, dtype=np.uint8)
+    out = np.empty((n_vals, val_len), dtype=np.uint8)
+    for i in range(n_vals):
+        pos = 0
+        row = out[i]
+        while pos < val_len:
+            if rng.random() < fresh:
+                ln = int(rng.integers(1, 16))
+                row[pos:pos + ln] = rng.integers(0, 256, size=min(ln, val_len - pos), dtype=np.uint8)
+            else:
+                ln = int(rng.integers(4, 64))
+                st = int(rng.integers(0, dict_size - ln))
+                m = min(ln, val_len - pos)
+                row[pos:pos + m] = d[st:st + m]
+            pos += ln
+    return out

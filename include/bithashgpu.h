@@ -1,0 +1,208 @@
+/*
+ * bithashgpu.h -- C-ABI of the MI355X (gfx950) bithash block codec.
+ *
+ * This is the drop-in boundary a Go (cgo) caller binds.
+ * Plain C types only: pointers, sizes, PODs.  No HIP/torch types appear in
+ * any signature; streams are passed as opaque `void*` (a hipStream_t, or
+ * NULL for the context's own stream).
+ *
+ * A "bithash block" is one data record of a .bht table file
+ * (bithash/block2.go:26,31-36,73-105):
+ *
+ *     u32 ikeySize | u32 valueSize | u32 fileNum | ikey[ikeySize] | value[valueSize]
+ *     ikey = userKey || u64 LE trailer (seq<<8 | kind)     (internal/base/internal.go:67-72,121-124)
+ *
+ * addressed by BlockHandle{Offset u32, Length u32} (bithash/block.go:26-39).
+ * Blocks are independent: the batch entry points decode/encode N of them in
+ * one launch sequence.  Unless a function says otherwise, every buffer
+ * pointer is DEVICE memory (device-resident path); *_host variants take
+ * host memory and include the H2D/D2H copies (end-to-end path).
+ *
+ * Ownership: the library never frees caller memory.  Device scratch is owned
+ * by the bhg_ctx.  Errors: functions return 0 (BHG_OK) or a negative
+ * BHG_E* code; bhg_last_error() gives the text.  Nothing aborts or throws
+ * across this boundary.  Per-block outcomes are reported in status columns
+ * (BHG_ST_*), mapped 1:1 onto the reference's Go errors.
+ *
+ * Threading: a bhg_ctx may be used from several host threads on distinct
+ * streams; calls on one stream are ordered.  Multi-GPU: one ctx per device.
+ */
+#ifndef BITHASHGPU_H
+#define BITHASHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BHG_ABI_VERSION 1
+
+/* ---- API return codes ---- */
+#define BHG_OK 0
+#define BHG_EINVAL (-1)     /* bad argument (null pointer, n too large, bad codec) */
+#define BHG_EHIP (-2)       /* HIP runtime error */
+#define BHG_ENOMEM (-3)     /* device allocation failed */
+#define BHG_ENODEV (-4)     /* no such device / no GPU */
+#define BHG_ECAPACITY (-5)  /* caller output buffer too small */
+
+/* ---- codecs: internal/compress/compress.go:21-24 (CompressTypeNo / CompressTypeSnappy) ---- */
+#define BHG_CODEC_NONE 0
+#define BHG_CODEC_SNAPPY 1
+
+/* ---- per-block status (decode) / per-record status (encode) ---- */
+#define BHG_ST_OK 0
+#define BHG_ST_RECORD_NIL 1        /* readRecord -> nil: ErrBhReadRecordNil (block2.go:57-66, reader.go:260-264, error.go) */
+#define BHG_ST_ILLEGAL_LENGTH 2    /* bh.Length <= 0: ErrBhIllegalBlockLength (reader.go:234-236) */
+#define BHG_ST_INCOMPLETE 3        /* handle past end of src: ReadAt short / io.EOF (reader.go:251-258) */
+#define BHG_ST_SNAPPY_CORRUPT 4    /* snappy.ErrCorrupt (compress.go:83-85) */
+#define BHG_ST_SNAPPY_TOO_LARGE 5  /* decoded length exceeds the output slot given to the block */
+#define BHG_ST_CRC_MISMATCH 6      /* build extension: expected_crc given and != computed */
+#define BHG_ST_KEY_TOO_LARGE 7     /* ErrBhKeyTooLarge  (writer.go:260-261) */
+#define BHG_ST_VALUE_TOO_LARGE 8   /* ErrBhValueTooLarge (writer.go:262-263) */
+#define BHG_ST_DATA_MAX_EXCEEDED 9 /* "bithash: panic add exceed data max size" (writer.go:266-269) */
+
+/* BlockHandle (block.go:26-39) with the offset widened to 64 bits so one
+ * batch may span many concatenated/mmap'd table files. 16 B. */
+typedef struct bhg_handle {
+    uint64_t offset;
+    uint32_t length;
+    uint32_t pad;
+} bhg_handle;
+
+/* One decoded block (40 B).  Mirrors readRecord's (*InternalKey, value,
+ * FileNum) (block2.go:57-66) plus the build's CRC column:
+ *   key_off/key_len : UserKey view, relative to the record start (12, ikeySize-8);
+ *                     key_len = 0 when ikeySize < 8 (UserKey nil)
+ *   val_off/val_len : codec NONE -> zero-copy value view relative to the record
+ *                     start (noCompressor.Decode returns src, compress.go:57-59);
+ *                     codec SNAPPY -> val_off = 0, val_len = decoded length, the
+ *                     bytes at out_vals + out_val_off[i]
+ *   trailer         : ikey trailer u64 (seq<<8|kind); 255 (InternalKeyKindInvalid)
+ *                     when ikeySize < 8 (base.DecodeInternalKey)
+ *   file_num        : header fileNum
+ *   fnv1            : hash.Fnv32(UserKey) (internal/hash/fnv.go:19-23, FNV-1)
+ *   crc             : crc.New(record[0:L]).Value() -- masked CRC-32C (internal/crc/crc.go:19-33)
+ *                     computed whenever the handle lies inside src
+ *   status          : BHG_ST_*
+ * For RECORD_NIL / ILLEGAL_LENGTH / INCOMPLETE every field except crc and
+ * status is 0.  For SNAPPY_* the key fields are filled, val_off/val_len 0. */
+typedef struct bhg_desc {
+    uint32_t key_off, key_len;
+    uint32_t val_off, val_len;
+    uint64_t trailer;
+    uint32_t file_num;
+    uint32_t fnv1;
+    uint32_t crc;
+    uint32_t status;
+} bhg_desc;
+
+typedef struct bhg_ctx bhg_ctx;
+
+/* ---- context / device ---- */
+int bhg_abi_version(void);
+int bhg_device_count(void);
+/* device: HIP ordinal; flags: reserved (0).  Returns NULL on failure. */
+bhg_ctx *bhg_create(int device, int flags);
+void bhg_destroy(bhg_ctx *ctx);
+const char *bhg_last_error(const bhg_ctx *ctx);
+/* the context's own stream (a hipStream_t) */
+void *bhg_stream(bhg_ctx *ctx);
+int bhg_stream_sync(bhg_ctx *ctx, void *stream);
+
+/* ---- memory helpers (so a cgo caller needs no HIP headers) ---- */
+void *bhg_malloc_device(bhg_ctx *ctx, uint64_t bytes);
+int bhg_free_device(bhg_ctx *ctx, void *p);
+void *bhg_malloc_host(bhg_ctx *ctx, uint64_t bytes); /* pinned */
+int bhg_free_host(bhg_ctx *ctx, void *p);
+int bhg_memcpy_h2d(bhg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int bhg_memcpy_d2h(bhg_ctx *ctx, void *dst, const void *src, uint64_t bytes, void *stream);
+int bhg_memset_device(bhg_ctx *ctx, void *dst, int value, uint64_t bytes, void *stream);
+
+/* ---- batch decode (device-resident) ----
+ * Replaces, per block, Reader.readData's readRecord + compressor.Decode
+ * (bithash/reader.go:233-272, bithash/writer.go:215-222 for open tables,
+ * block2.go:57-66, compress.go:57-59 / 83-85), batched; adds FNV-1 of the
+ * user key (hash.Fnv32, needed by Writer.rebuild writer.go:575 and compaction
+ * bitree/bithash.go:224) and the masked CRC-32C of the record.
+ *   src, src_len     : bytes the handles index into (e.g. concatenated .bht files)
+ *   handles[n]       : block handles (offset relative to src)
+ *   codec            : BHG_CODEC_NONE or BHG_CODEC_SNAPPY
+ *   expected_crc     : nullable; if given, mismatching OK blocks -> BHG_ST_CRC_MISMATCH
+ *   out_desc[n]      : descriptors
+ *   SNAPPY only:
+ *   out_val_off[n+1] : written by the library: exclusive scan of the decoded
+ *                      lengths; out_val_off[n] = total bytes needed
+ *   out_vals, out_vals_cap : decoded values; a block whose slot would end past
+ *                      out_vals_cap gets BHG_ST_SNAPPY_TOO_LARGE
+ * Asynchronous on `stream`.  All pointers device memory. */
+int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
+                     uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
+                     uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off, void *stream);
+
+/* Same contract with HOST buffers (may be pageable or bhg_malloc_host):
+ * copies in, decodes, copies out; synchronous.  This is the end-to-end
+ * path (mmap'd .bht -> H2D -> kernel -> D2H). */
+int bhg_decode_batch_host(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
+                          uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
+                          uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off);
+
+/* ---- primitives, batched (device) ----
+ * crc.New(src[h.offset : h.offset+h.length]).Value() for each handle
+ * (internal/crc/crc.go:23-33; the indexhash_checksum of writer.go:477 is one
+ * such range).  Handles past src_len give 0. */
+int bhg_crc32c_masked_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
+                            uint32_t n, uint32_t *out_crc, void *stream);
+/* hash.Fnv32 of each range (internal/hash/fnv.go:19-23) */
+int bhg_fnv32_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
+                    uint32_t n, uint32_t *out_fnv, void *stream);
+
+/* ---- batch encode (device-resident): BithashWriter.Add over N pairs ----
+ * Replaces Writer.Add/add (bithash/writer.go:230-283) + block2Writer.set
+ * (block2.go:73-105) + compressor.Encode (compress.go:67-69) + hash.Fnv32 +
+ * maybeSplitTable (bithash_writer.go:47-67), batched:
+ *   keys, key_off[n+1]      : concatenated user keys
+ *   trailers[n]             : ikey trailers (seq<<8 | kind)
+ *   vals, val_off[n+1]      : concatenated raw values
+ *   codec                   : BHG_CODEC_NONE / BHG_CODEC_SNAPPY (golang/snappy v0.0.4 Encode)
+ *   file_nums[max_tables]   : fileNum of table 0,1,2... (header fileNum of its records)
+ *   init_size               : meta.Size/currentOffset of table 0 when the batch starts
+ *   table_max               : TableMaxSize; after each successful add,
+ *                             size >= table_max starts the next table at 0
+ *   out, out_cap            : packed records of all tables, concatenated
+ * Outputs (device arrays, n entries unless noted) in bhg_encode_out. */
+typedef struct bhg_encode_out {
+    uint64_t *pos;          /* byte position of record i in out (UINT64_MAX if its add failed) */
+    uint32_t *bh_off;       /* BlockHandle.Offset inside its table */
+    uint32_t *bh_len;       /* BlockHandle.Length */
+    uint32_t *table;        /* table index (0-based) */
+    uint32_t *fnv1;         /* hash.Fnv32(userKey) */
+    uint32_t *crc;          /* masked CRC-32C of the packed record */
+    uint32_t *status;       /* BHG_ST_OK / KEY_TOO_LARGE / VALUE_TOO_LARGE / DATA_MAX_EXCEEDED */
+    uint32_t *table_start;  /* [max_tables] first record index of each table */
+    uint64_t *summary;      /* [4]: total bytes written, tables used, failed adds, reserved */
+} bhg_encode_out;
+
+int bhg_encode_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                     const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                     const uint32_t *file_nums, uint32_t max_tables, uint32_t init_size, uint64_t table_max,
+                     uint8_t *out, uint64_t out_cap, const bhg_encode_out *o, void *stream);
+
+/* ---- table data-region scan (device) ----
+ * TableIterator.findEntry (bithash/table.go:358-395, mode 0) or Writer.rebuild
+ * (bithash/writer.go:539-583, mode 1) over each table: the sequential header
+ * chase that yields every record's handle in file order.
+ *   src, table_off[ntables+1] : table files concatenated; table t = src[table_off[t] : table_off[t+1]]
+ *   out_handles, max_out      : handles (offset relative to src), table t's
+ *                               records start at out_first[t]
+ *   out_first[ntables+1]      : written: exclusive scan of per-table counts
+ *   out_end[ntables]          : written: offset (inside table) where the scan stopped */
+int bhg_scan_tables(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                    bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
+                    void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BITHASHGPU_H */

@@ -139,8 +139,14 @@ def record_set(ukey, trailer, value, file_num):
     return out[:m].tobytes()
 
 
+def _u8(src):
+    if isinstance(src, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(src), dtype=np.uint8)
+    return np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+
+
 def decode_sizes(src, handles):
-    src = np.ascontiguousarray(src, dtype=np.uint8)
+    src = _u8(src)
     handles = np.ascontiguousarray(handles, dtype=HANDLE_DT)
     out = np.zeros(len(handles), dtype=np.uint64)
     lib().bho_decode_sizes(_ptr(src), src.size, _ptr(handles), len(handles), _ptr(out))
@@ -152,7 +158,7 @@ def decode_batch(src, handles, codec=0, expected_crc=None, nthreads=0, out_val_o
 
     nthreads=0: single thread, reference-definition CRC (checker mode);
     nthreads>=1: threaded, SSE4.2 CRC (baseline mode)."""
-    src = np.ascontiguousarray(src, dtype=np.uint8)
+    src = _u8(src)
     handles = np.ascontiguousarray(handles, dtype=HANDLE_DT)
     n = len(handles)
     desc = np.zeros(n, dtype=DESC_DT)

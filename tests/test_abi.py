@@ -1,0 +1,58 @@
+"""CPU-side checks of the C-ABI library: it builds, loads, and exports every
+symbol include/bithashgpu.h declares (no compute calls without a GPU)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from bitalosdb_amd import _lib as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "bithashgpu.h")).read()
+    return sorted(set(re.findall(r"\b(bhg_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_builds_and_loads():
+    B.build()
+    assert os.path.exists(B.LIB_PATH)
+    L = B.lib()
+    assert L.bhg_abi_version() == 1
+
+
+def test_exports_match_header():
+    B.build()
+    syms = header_symbols()
+    assert set(syms) == set(B.EXPORTS)
+    out = subprocess.check_output(["nm", "-D", "--defined-only", B.LIB_PATH]).decode()
+    exported = set(re.findall(r"\bT (bhg_[a-z0-9_]+)", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+
+
+def test_no_torch_types_in_header():
+    txt = open(os.path.join(ROOT, "include", "bithashgpu.h")).read()
+    code = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)       # declarations only, comments stripped
+    code = re.sub(r"//[^\n]*", "", code)
+    for bad in ("torch", "at::", "hipStream_t", "Tensor", "#include <hip"):
+        assert bad not in code
+
+
+def test_struct_layouts():
+    assert B.HANDLE_DT.itemsize == 16
+    assert B.DESC_DT.itemsize == 40
+    assert B.DESC_DT.fields["trailer"][1] == 16
+    assert B.DESC_DT.fields["status"][1] == 36
+
+
+def test_no_device_means_no_context():
+    # this container has no GPU: the library must refuse, not fall back to a CPU path
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = B.lib()
+    assert L.bhg_device_count() == 0
+    assert not L.bhg_create(0, 0)
