@@ -81,7 +81,17 @@ def main():
     from bitalosdb_amd.codec import BithashCodec, handles_tensor
     _lib.lib()
     codec = BithashCodec(local)
+    with torch.cuda.stream(codec.stream):      # every torch op and event on the codec's HIP stream
+        run(a, world, rank, local, dev, codec)
+    codec.close()
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def run(a, world, rank, local, dev, codec):
+    import torch.distributed as dist
+    from bitalosdb_amd import synth
+    from bitalosdb_amd.codec import handles_tensor
     n = a.blocks
     # rank r owns its own tables (round-robin by table file: file numbers disjoint per rank)
     src_t, h, meta = synth.uniform_tables(n, device=dev, seed=synth.SEED + rank,
@@ -206,9 +216,6 @@ def main():
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    codec.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

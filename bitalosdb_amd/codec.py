@@ -96,6 +96,9 @@ class BithashCodec:
         self.ctx = self.L.bhg_create(device, 0)
         if not self.ctx:
             raise B.BhgError("bhg_create(%d) failed" % device)
+        # torch work for this codec (allocations, copies, events) runs on the
+        # context's own HIP stream, so every launch is ordered with it
+        self.stream = torch.cuda.ExternalStream(self.L.bhg_stream(self.ctx), device=self.device)
 
     def close(self):
         if self.ctx:
@@ -109,10 +112,10 @@ class BithashCodec:
             pass
 
     def _stream(self):
-        return torch.cuda.current_stream(self.device).cuda_stream
+        return self.stream.cuda_stream
 
     def sync(self):
-        torch.cuda.current_stream(self.device).synchronize()
+        self.stream.synchronize()
 
     # ---- decode ----
     def decode_batch(self, src, src_len, handles, n, compressor=NoCompressor, expected_crc=None,
@@ -138,6 +141,10 @@ class BithashCodec:
     def decode(self, src, handles, compressor=NoCompressor, expected_crc=None):
         """Convenience: host arrays in, device decode, results as numpy.
         Snappy runs two passes: sizes -> allocate -> decode (the library fills val_off)."""
+        with torch.cuda.stream(self.stream):
+            return self._decode(src, handles, compressor, expected_crc)
+
+    def _decode(self, src, handles, compressor, expected_crc):
         dev = self.device
         src_t = as_device_bytes(src, dev)
         h_t = handles_tensor(handles, dev)
@@ -178,14 +185,16 @@ class BithashCodec:
 
     # ---- primitives ----
     def crc_batch(self, src_t, handles_t, n):
-        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.stream(self.stream):
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
         rc = self.L.bhg_crc32c_masked_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(out),
                                             self._stream())
         B.check(self.ctx, rc, "bhg_crc32c_masked_batch")
         return out
 
     def fnv_batch(self, src_t, handles_t, n):
-        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.stream(self.stream):
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
         rc = self.L.bhg_fnv32_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(out),
                                     self._stream())
         B.check(self.ctx, rc, "bhg_fnv32_batch")

@@ -105,7 +105,9 @@ bhg_ctx *bhg_create(int device, int flags) {
     c->lane_wgs_per_cu = 4;
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
     c->err[0] = 0;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // blocking stream: orders against the legacy NULL stream, so callers that
+    // stage buffers on the default stream need no extra event
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
         delete c;
         return nullptr;
     }

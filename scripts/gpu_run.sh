@@ -1,0 +1,41 @@
+#!/bin/bash
+# GPU-box driver: parity tests, bench, rocprofv3 kernel-trace summary.
+# usage: bash scripts/gpu_run.sh <tag> [steps...]   (each GPU step under its own timeout, chained)
+set -o pipefail
+TAG=${1:-run}
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+nproc > $OUT/nproc.txt
+grep -m1 "model name" /proc/cpuinfo > $OUT/cpu.txt
+shift
+STEPS=${@:-"test bench prof"}
+for s in $STEPS; do
+  case $s in
+    test)
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?
+      echo "pytest rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
+      [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+      cat $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $OUT/bench.log 2>&1 || exit $?
+      cat $OUT/bench.log ;;
+    benchq)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu --no-e2e > $OUT/benchq.log 2>&1 || exit $?
+      cat $OUT/benchq.log ;;
+    prof)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu --no-e2e > $OUT/prof.log 2>&1 || exit $?
+      find $OUT/prof -name "*stats*" | head ;;
+    pmc)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/$OUT/pmc1 -o run --output-format csv \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $OUT/pmc1.log 2>&1 || exit $?
+      timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $GRAFT_REPO_ROOT/$OUT/pmc2 -o run --output-format csv \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $OUT/pmc2.log 2>&1 || exit $? ;;
+  esac
+done
+echo done

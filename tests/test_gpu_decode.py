@@ -256,6 +256,11 @@ def test_full_size_c2_parity(codec):
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import handles_tensor
     n = 1_000_000
+    with torch.cuda.stream(codec.stream):
+        _full_size(codec, synth, handles_tensor, n)
+
+
+def _full_size(codec, synth, handles_tensor, n):
     src_t, h, meta = synth.uniform_tables(n, device=codec.device)
     assert meta["tables"] == 9 and meta["records_per_table"] == 124738
     dh = handles_tensor(h, codec.device)
