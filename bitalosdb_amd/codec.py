@@ -207,3 +207,76 @@ def read_record_status(desc_row):
     if int(desc_row["status"]) != B.ST_OK:
         raise BithashCodecError(desc_row["status"])
     return (int(desc_row["key_off"]), int(desc_row["key_len"]), int(desc_row["val_off"]), int(desc_row["val_len"]))
+
+
+def _u64_tensor(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64).copy()).to(device)
+
+
+def _u32_tensor(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32).copy()).to(device)
+
+
+class EncodeBuffers:
+    """Device outputs of bhg_encode_batch (bhg_encode_out)."""
+
+    def __init__(self, n, max_tables, device):
+        z = lambda k, dt: torch.zeros(k, dtype=dt, device=device)
+        self.pos = z(n, torch.int64)
+        self.bh_off = z(n, torch.int32)
+        self.bh_len = z(n, torch.int32)
+        self.table = z(n, torch.int32)
+        self.fnv1 = z(n, torch.int32)
+        self.crc = z(n, torch.int32)
+        self.status = z(n, torch.int32)
+        self.table_start = z(max_tables, torch.int32)
+        self.summary = z(4, torch.int64)
+
+    def struct(self):
+        return B.EncodeOut(*[_ptr(getattr(self, f)) for f, _ in B.EncodeOut._fields_])
+
+
+def _encode_codec(self, keys_t, key_off_t, trailers_t, vals_t, val_off_t, n, codec, file_nums_t, max_tables,
+                  init_size, table_max, out_t, bufs, stream=None):
+    """Device-resident bhg_encode_batch (all tensors on the codec's device)."""
+    o = bufs.struct()
+    rc = self.L.bhg_encode_batch(self.ctx, _ptr(keys_t), _ptr(key_off_t), _ptr(trailers_t), _ptr(vals_t),
+                                 _ptr(val_off_t), n, codec, _ptr(file_nums_t), max_tables, init_size, table_max,
+                                 _ptr(out_t), out_t.numel(), ctypes.byref(o),
+                                 stream if stream is not None else self._stream())
+    B.check(self.ctx, rc, "bhg_encode_batch")
+    return bufs
+
+
+def _encode(self, keys, trailers, values, compressor=NoCompressor, file_nums=(1,), init_size=0,
+            table_max=128 << 20, out_cap=None):
+    """BithashWriter.Add over a host batch (lists of bytes); results as numpy (oracle-shaped dict)."""
+    dev = self.device
+    with torch.cuda.stream(self.stream):
+        n = len(keys)
+        key_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(k) for k in keys], out=key_off[1:])
+        val_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(v) for v in values], out=val_off[1:])
+        kb = as_device_bytes(b"".join(keys) or b"\0", dev)
+        vb = as_device_bytes(b"".join(values) or b"\0", dev)
+        if out_cap is None:
+            out_cap = int(sum(20 + len(k) + len(v) + len(v) // 6 + 32 for k, v in zip(keys, values))) + 16
+        out = torch.zeros(max(out_cap, 1), dtype=torch.uint8, device=dev)
+        bufs = EncodeBuffers(n, len(file_nums), dev)
+        self.encode_batch(kb, _u64_tensor(key_off, dev), _u64_tensor(trailers, dev), vb, _u64_tensor(val_off, dev),
+                          n, compressor, _u32_tensor(file_nums, dev), len(file_nums), init_size, table_max, out, bufs)
+        self.sync()
+        summ = bufs.summary.cpu().numpy().view(np.uint64)
+        nt = int(summ[1])
+        if nt == 0:
+            raise ValueError("not enough file numbers for the table splits")
+        total = int(summ[0])
+        u32 = lambda t: t.cpu().numpy().view(np.uint32)
+        return dict(out=out[:total].cpu().numpy(), pos=bufs.pos.cpu().numpy().view(np.uint64), bh_off=u32(bufs.bh_off),
+                    bh_len=u32(bufs.bh_len), table=u32(bufs.table), fnv=u32(bufs.fnv1), crc=u32(bufs.crc),
+                    status=u32(bufs.status), table_start=u32(bufs.table_start)[:nt], ntables=nt)
+
+
+BithashCodec.encode_batch = _encode_codec
+BithashCodec.encode = _encode

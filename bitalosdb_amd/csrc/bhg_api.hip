@@ -19,6 +19,7 @@ struct bhg_ctx {
     hipStream_t stream;
     int num_cus;
     int lane_wgs_per_cu;
+    int variant;
     char err[512];
     std::mutex mu;          // guards scratch growth and the host-path buffers
     void *scratch = nullptr;
@@ -54,6 +55,7 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     L.stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     L.num_cus = c->num_cus;
     L.lane_wgs_per_cu = c->lane_wgs_per_cu;
+    L.variant = c->variant;
     return L;
 }
 
@@ -102,8 +104,10 @@ bhg_ctx *bhg_create(int device, int flags) {
     bhg_ctx *c = new bhg_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    c->lane_wgs_per_cu = 4;
+    c->lane_wgs_per_cu = 0;
+    c->variant = 1;
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
+    if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
     c->err[0] = 0;
     // blocking stream: orders against the legacy NULL stream, so callers that
     // stage buffers on the default stream need no extra event
@@ -278,6 +282,53 @@ int bhg_fnv32_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_
     if (!handles || !out_fnv || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     HIP_TRY(c, bhg::launch_fnv_ranges(launch_of(c, stream), src, src_len, handles, n, out_fnv));
+    return BHG_OK;
+}
+
+int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                     const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec, const uint32_t *file_nums,
+                     uint32_t max_tables, uint32_t init_size, uint64_t table_max, uint8_t *out, uint64_t out_cap,
+                     const bhg_encode_out *o, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (!o || !o->table_start || !o->summary || max_tables < 1 || !file_nums) { set_err(c, "bad encode outputs"); return BHG_EINVAL; }
+    if (codec != BHG_CODEC_NONE && codec != BHG_CODEC_SNAPPY) { set_err(c, "bad codec %d", codec); return BHG_EINVAL; }
+    // DATA_MAX_EXCEEDED (writer.go:266-269) cannot trigger when size < table_max and
+    // table_max + max record <= dataMaxSize; larger tables are rejected up front.
+    const uint64_t data_max = 0xFFFFFFFFull - (256ull << 20);
+    if (table_max == 0 || table_max + (33ull << 10) + (256ull << 20) + 12 > data_max || init_size >= table_max) {
+        set_err(c, "table_max/init_size out of range");
+        return BHG_EINVAL;
+    }
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    if (n == 0) {
+        HIP_TRY(c, hipMemsetAsync(o->summary, 0, 32, L.stream));
+        uint64_t one = 1;
+        HIP_TRY(c, hipMemcpyAsync(o->summary + 1, &one, 8, hipMemcpyHostToDevice, L.stream));
+        HIP_TRY(c, hipMemsetAsync(o->table_start, 0, 4, L.stream));
+        return BHG_OK;
+    }
+    if (!keys || !key_off || !trailers || !vals || !val_off || !out || !o->pos || !o->bh_off || !o->bh_len ||
+        !o->table || !o->fnv1 || !o->crc || !o->status) {
+        set_err(c, "null buffer");
+        return BHG_EINVAL;
+    }
+    if (codec == BHG_CODEC_SNAPPY) { set_err(c, "snappy encode: not built in this version"); return BHG_EINVAL; }
+    std::lock_guard<std::mutex> g(c->mu);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t lens_b = al(((size_t)n + 1) * 8), vlen_b = al((size_t)n * 8), scan_b = al(bhg::scan_scratch_bytes(n));
+    if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, lens_b + vlen_b + scan_b)) return r;
+    uint8_t *sp = reinterpret_cast<uint8_t *>(c->scratch);
+    bhg::EncodeLaunch E;
+    E.lens = reinterpret_cast<uint64_t *>(sp);
+    uint64_t *vlen = reinterpret_cast<uint64_t *>(sp + lens_b);
+    E.scan_scratch = sp + lens_b + vlen_b;
+    HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
+    E.keys = keys; E.key_off = key_off; E.trailers = trailers;
+    E.vbase = vals; E.vpos = val_off; E.vlen = vlen;
+    E.n = n; E.file_nums = file_nums; E.max_tables = max_tables; E.init_size = init_size; E.table_max = table_max;
+    E.out = out; E.out_cap = out_cap; E.o = *o;
+    HIP_TRY(c, bhg::launch_encode(L, E));
     return BHG_OK;
 }
 

@@ -55,7 +55,7 @@ __device__ __forceinline__ void crc_lds_fill(uint32_t *T) {
     }
 }
 
-// Per-lane view of the replicated table.
+// Per-lane view of the replicated byte table (slice-by-1).
 struct CrcLds {
     const uint32_t *t;  // T + (lane & 31)
     __device__ __forceinline__ explicit CrcLds(const uint32_t *T) : t(T + (threadIdx.x & 31)) {}
@@ -77,6 +77,78 @@ struct CrcLds {
         }
         return c;
     }
+};
+
+// Slice-by-4 tables T0..T3 (T_{k+1}[i] = T_k[i] >> 8 ^ T0[T_k[i] & 0xff]),
+// each replicated R times and interleaved so that lane l reads copy (l % R):
+// dword index = k*256*R + i*R + (l % R).  R = 32 is bank-conflict free for
+// ds_read_b32 (128 KiB); smaller R trades LDS for bank conflicts among the
+// 32/R lanes that share a copy.  One word costs 4 independent lookups, so
+// the dependent LDS chain is one round trip per 4 bytes instead of 4.
+template <int R>
+struct Crc4Lds {
+    static constexpr int kLog = R == 32 ? 5 : R == 16 ? 4 : R == 8 ? 3 : R == 4 ? 2 : R == 2 ? 1 : 0;
+    static constexpr uint32_t kWords = 4u * 256u * R;
+    static constexpr uint32_t kShift = 2 + kLog;  // idx -> byte offset
+    const uint8_t *base;
+    uint32_t lb0, lb1, lb2, lb3;  // per-table lane base byte offsets
+    __device__ __forceinline__ explicit Crc4Lds(const uint32_t *T) : base(reinterpret_cast<const uint8_t *>(T)) {
+        const uint32_t lo = (threadIdx.x & (R - 1)) * 4;
+        lb0 = lo;
+        lb1 = lo + 1u * 1024u * R;
+        lb2 = lo + 2u * 1024u * R;
+        lb3 = lo + 3u * 1024u * R;
+    }
+    __device__ __forceinline__ uint32_t ld(uint32_t off) const {
+        return *reinterpret_cast<const uint32_t *>(base + off);
+    }
+    // lookup table k at byte (x >> sh) & 0xff; offsets of (idx << kShift) never overlap the lane bits
+    __device__ __forceinline__ uint32_t word(uint32_t c, uint32_t w) const {
+        const uint32_t x = c ^ w;
+        const uint32_t m = 0xffu << kShift;
+        const uint32_t a3 = ((x << kShift) & m) | lb3;
+        const uint32_t a2 = ((x >> (8 - kShift)) & m) | lb2;
+        const uint32_t a1 = ((x >> (16 - kShift)) & m) | lb1;
+        const uint32_t a0 = ((x >> (24 - kShift)) & m) | lb0;
+        return ld(a3) ^ ld(a2) ^ ld(a1) ^ ld(a0);
+    }
+    __device__ __forceinline__ uint32_t step(uint32_t c) const {  // one byte via T0
+        return (c >> 8) ^ ld(((c & 0xffu) << kShift) | lb0);
+    }
+    __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const {
+        uint32_t m = nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
+        c ^= x & m;
+#pragma unroll
+        for (uint32_t s = 0; s < 4; s++) {
+            uint32_t n = step(c);
+            c = s < nb ? n : c;
+        }
+        return c;
+    }
+    // fill all 4 tables (whole workgroup)
+    static __device__ __forceinline__ void fill(uint32_t *T) {
+        for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+            uint32_t t[4];
+            t[0] = crc_table_entry(i);
+#pragma unroll
+            for (int k = 1; k < 4; k++) t[k] = (t[k - 1] >> 8) ^ crc_table_entry(t[k - 1] & 0xffu);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t *dst = T + (uint32_t)k * 256u * R + i * R;
+#pragma unroll
+                for (int r = 0; r < R; r++) dst[r] = t[k];
+            }
+        }
+    }
+};
+
+// DIAGNOSTIC ONLY (variant table entries marked diag): a "table" that folds
+// words with xor/rotate instead of CRC lookups -- isolates the memory side of
+// the lane kernels.  Never selected by default; outputs are not CRCs.
+struct XorTab {
+    __device__ __forceinline__ explicit XorTab(const uint32_t *) {}
+    __device__ __forceinline__ uint32_t word(uint32_t c, uint32_t w) const { return ((c << 1) | (c >> 31)) ^ w; }
+    __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const { return word(c, x + nb); }
 };
 
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) {  // crc.go:31-33
@@ -110,11 +182,14 @@ __device__ __forceinline__ uint64_t ldu64(uint64_t p, uint64_t end) {
 
 // Raw CRC-32C chain (Go crc32.Update internals: state already inverted) over
 // the absolute byte range [p, p+len), every load kept below `end`.
-// One lane walks its own range; 64 B per iteration via 4 dword-aligned
-// dwordx4 loads, next window prefetched while the current one is absorbed.
-__device__ __forceinline__ uint32_t crc_range(const CrcLds &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
+// One lane walks its own range in windows of WIN x 16 B, loaded by WIN
+// dword-aligned dwordx4 loads issued back to back so that a lane consumes
+// whole cache lines while they are L1-resident (lanes of a wave walk
+// different records: a 16 B-per-lane burst would cost one L2 request per
+// 16 B).  PREFETCH keeps the next window in flight while absorbing.
+template <int WIN, bool PREFETCH, class Tab>
+__device__ __forceinline__ uint32_t crc_range_w(const Tab &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
     if (len == 0) return c;
-    // head: bytes up to the next 4-aligned address
     uint64_t a0 = p & ~3ull;
     uint32_t z = (uint32_t)(p & 3);
     if (z) {
@@ -126,41 +201,37 @@ __device__ __forceinline__ uint32_t crc_range(const CrcLds &T, uint32_t c, uint6
         len -= nb;
         if (len == 0) return c;
     }
-    // p is 4-aligned now
-    uint64_t nw = len >> 2;
-    uint32_t tail = (uint32_t)(len & 3);
-    uint64_t a = p;
+    const uint64_t nw = len >> 2;
+    const uint32_t tail = (uint32_t)(len & 3);
+    const uint64_t a = p;
+    constexpr uint32_t WW = 4 * WIN;  // words per window
     if (nw) {
-        const bool fast0 = a + 64 <= end;
-        u32x4 cur[4], nxt[4];
+        u32x4 cur[WIN], nxt[PREFETCH ? WIN : 1];
+        auto load_win = [&](u32x4 *dst, uint64_t at) {
+            if (at + 16 * WIN <= end) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (fast0) cur[q] = gld<u32x4_a4>(a + 16 * q);
-            else cur[q] = u32x4{ld32_safe(a + 16 * q, end), ld32_safe(a + 16 * q + 4, end),
-                                ld32_safe(a + 16 * q + 8, end), ld32_safe(a + 16 * q + 12, end)};
-        }
-        for (uint64_t base = 0; base < nw; base += 16) {
-            const uint64_t an = a + 64 * (base / 16 + 1);
-            const bool more = base + 16 < nw;
-            if (more) {
-                const bool fast = an + 64 <= end;
+                for (int q = 0; q < WIN; q++) dst[q] = gld<u32x4_a4>(at + 16 * q);
+            } else {
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (fast) nxt[q] = gld<u32x4_a4>(an + 16 * q);
-                    else nxt[q] = u32x4{ld32_safe(an + 16 * q, end), ld32_safe(an + 16 * q + 4, end),
-                                        ld32_safe(an + 16 * q + 8, end), ld32_safe(an + 16 * q + 12, end)};
-                }
+                for (int q = 0; q < WIN; q++)
+                    dst[q] = u32x4{ld32_safe(at + 16 * q, end), ld32_safe(at + 16 * q + 4, end),
+                                   ld32_safe(at + 16 * q + 8, end), ld32_safe(at + 16 * q + 12, end)};
             }
+        };
+        load_win(cur, a);
+        for (uint64_t base = 0; base < nw; base += WW) {
+            const bool more = base + WW < nw;
+            if (PREFETCH && more) load_win(nxt, a + 4 * (base + WW));
             const uint64_t rem = nw - base;
-            if (rem >= 16) {
+            if (rem >= WW) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < WIN; q++) {
                     c = T.word(c, cur[q].x); c = T.word(c, cur[q].y);
                     c = T.word(c, cur[q].z); c = T.word(c, cur[q].w);
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < WIN; q++) {
                     if ((uint64_t)(4 * q + 0) < rem) c = T.word(c, cur[q].x);
                     if ((uint64_t)(4 * q + 1) < rem) c = T.word(c, cur[q].y);
                     if ((uint64_t)(4 * q + 2) < rem) c = T.word(c, cur[q].z);
@@ -168,13 +239,226 @@ __device__ __forceinline__ uint32_t crc_range(const CrcLds &T, uint32_t c, uint6
                 }
             }
             if (more) {
+                if (PREFETCH) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+                    for (int q = 0; q < WIN; q++) cur[q] = nxt[q];
+                } else {
+                    load_win(cur, a + 4 * (base + WW));
+                }
             }
         }
     }
     if (tail) c = T.partial(c, ld32_safe(a + 4 * nw, end), tail);
     return c;
+}
+
+// Same chain with windows aligned to 128 B lines: the WIN x 16 B window
+// k covers [a0 + 16*WIN*k, +16*WIN) with a0 = (4-aligned start) & ~127, so a
+// cache line is requested by exactly one window of one lane (an unaligned
+// window straddles lines that are evicted before the next window asks for
+// them: 2x HBM over-fetch measured).  Words outside [pa, pe) are masked off;
+// the unaligned head/tail bytes are absorbed before/after the walk.
+template <int WIN, class Tab, bool PF = false>
+__device__ __forceinline__ uint32_t crc_range_a(const Tab &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
+    if (len == 0) return c;
+    const uint64_t pe_all = p + len;
+    const uint64_t pa = (p + 3) & ~3ull;
+    if (pa >= pe_all || pa + 4 > pe_all) {              // fewer than one aligned word: byte path
+        uint64_t q = p;
+        while (q < pe_all) {
+            const uint64_t a = q & ~3ull;
+            const uint32_t z = (uint32_t)(q & 3);
+            uint32_t nb = 4 - z;
+            if ((uint64_t)nb > pe_all - q) nb = (uint32_t)(pe_all - q);
+            c = T.partial(c, ld32_safe(a, end) >> (8 * z), nb);
+            q += nb;
+        }
+        return c;
+    }
+    if (pa != p) c = T.partial(c, ld32_safe(p & ~3ull, end) >> (8 * (uint32_t)(p & 3)), (uint32_t)(pa - p));
+    const uint64_t pe = pe_all & ~3ull;                // end of full words
+    constexpr uint32_t WB = 16 * WIN;
+    auto load_win = [&](u32x4 *cur, uint64_t w) {
+        if (w + WB <= end) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) cur[q] = gld<u32x4_a4>(w + 16 * q);
+        } else {
+#pragma unroll
+            for (int q = 0; q < WIN; q++)
+                cur[q] = u32x4{ld32_safe(w + 16 * q, end), ld32_safe(w + 16 * q + 4, end),
+                               ld32_safe(w + 16 * q + 8, end), ld32_safe(w + 16 * q + 12, end)};
+        }
+    };
+    const uint64_t w0 = pa & ~127ull;
+    u32x4 cur[WIN], nxt[PF ? WIN : 1];
+    if (w0 < pe) load_win(cur, w0);
+    for (uint64_t w = w0; w < pe; w += WB) {
+        const bool more = w + WB < pe;
+        if (PF && more) load_win(nxt, w + WB);
+        if (w >= pa && w + WB <= pe) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                c = T.word(c, cur[q].x); c = T.word(c, cur[q].y);
+                c = T.word(c, cur[q].z); c = T.word(c, cur[q].w);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const uint64_t b = w + 16 * q;
+                if (b + 0 >= pa && b + 0 < pe) c = T.word(c, cur[q].x);
+                if (b + 4 >= pa && b + 4 < pe) c = T.word(c, cur[q].y);
+                if (b + 8 >= pa && b + 8 < pe) c = T.word(c, cur[q].z);
+                if (b + 12 >= pa && b + 12 < pe) c = T.word(c, cur[q].w);
+            }
+        }
+        if (more) {
+            if (PF) {
+#pragma unroll
+                for (int q = 0; q < WIN; q++) cur[q] = nxt[q];
+            } else {
+                load_win(cur, w + WB);
+            }
+        }
+    }
+    if (pe != pe_all) c = T.partial(c, ld32_safe(pe, end), (uint32_t)(pe_all - pe));
+    return c;
+}
+
+// Line-aligned walk with an explicit two-buffer ping-pong (A/B): the loads
+// of window k+1 are issued before window k is absorbed and no register copy
+// joins the buffers, so the compiler's counted s_waitcnt vmcnt(N) keeps the
+// next window in flight (a cur = nxt copy made it wait for everything).
+template <int WIN, class Tab>
+__device__ __forceinline__ uint32_t crc_range_pp(const Tab &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
+    if (len == 0) return c;
+    const uint64_t pe_all = p + len;
+    const uint64_t pa = (p + 3) & ~3ull;
+    if (pa >= pe_all || pa + 4 > pe_all) {
+        uint64_t q = p;
+        while (q < pe_all) {
+            const uint64_t a = q & ~3ull;
+            const uint32_t z = (uint32_t)(q & 3);
+            uint32_t nb = 4 - z;
+            if ((uint64_t)nb > pe_all - q) nb = (uint32_t)(pe_all - q);
+            c = T.partial(c, ld32_safe(a, end) >> (8 * z), nb);
+            q += nb;
+        }
+        return c;
+    }
+    if (pa != p) c = T.partial(c, ld32_safe(p & ~3ull, end) >> (8 * (uint32_t)(p & 3)), (uint32_t)(pa - p));
+    const uint64_t pe = pe_all & ~3ull;
+    constexpr uint32_t WB = 16 * WIN;
+    auto load_win = [&](u32x4 *buf, uint64_t w) {
+        if (w + WB <= end) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) buf[q] = gld<u32x4_a4>(w + 16 * q);
+        } else {
+#pragma unroll
+            for (int q = 0; q < WIN; q++)
+                buf[q] = u32x4{ld32_safe(w + 16 * q, end), ld32_safe(w + 16 * q + 4, end),
+                               ld32_safe(w + 16 * q + 8, end), ld32_safe(w + 16 * q + 12, end)};
+        }
+    };
+    auto absorb = [&](const u32x4 *buf, uint64_t w) {
+        if (w >= pa && w + WB <= pe) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                c = T.word(c, buf[q].x); c = T.word(c, buf[q].y);
+                c = T.word(c, buf[q].z); c = T.word(c, buf[q].w);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const uint64_t b = w + 16 * q;
+                if (b + 0 >= pa && b + 0 < pe) c = T.word(c, buf[q].x);
+                if (b + 4 >= pa && b + 4 < pe) c = T.word(c, buf[q].y);
+                if (b + 8 >= pa && b + 8 < pe) c = T.word(c, buf[q].z);
+                if (b + 12 >= pa && b + 12 < pe) c = T.word(c, buf[q].w);
+            }
+        }
+    };
+    u32x4 A[WIN], Bf[WIN];
+    uint64_t w = pa & ~127ull;
+    if (w < pe) load_win(A, w);
+    while (w < pe) {
+        const uint64_t w1 = w + WB;
+        if (w1 < pe) load_win(Bf, w1);
+        absorb(A, w);
+        if (w1 >= pe) break;
+        const uint64_t w2 = w1 + WB;
+        if (w2 < pe) load_win(A, w2);
+        absorb(Bf, w1);
+        w = w2;
+    }
+    if (pe != pe_all) c = T.partial(c, ld32_safe(pe, end), (uint32_t)(pe_all - pe));
+    return c;
+}
+
+// Buffer-resource walk: windows are read with buffer_load_dwordx4 through a
+// wave-uniform descriptor (base, num_records) whose hardware range check
+// returns 0 past the end instead of faulting, so every load is issued
+// unconditionally (no fast/slow branch, no per-load guard) and the
+// compiler's counted vmcnt keeps window k+1 in flight while k is absorbed.
+// Windows are 128 B line-aligned; head/tail partial words come from the
+// same windows.  `rel` = absolute address - descriptor base (< 2^32).
+template <int WIN, class Tab>
+__device__ __forceinline__ uint32_t crc_range_buf(const Tab &T, uint32_t c, uint64_t p, uint64_t len,
+                                                  __amdgpu_buffer_rsrc_t rsrc, uint64_t rbase, uint32_t nwin_wave) {
+    const uint64_t pe_all = p + len;
+    const uint64_t pa = (p + 3) & ~3ull;
+    const uint64_t pe = pe_all & ~3ull;
+    const uint64_t hw = p & ~3ull;                 // head word (partial when p != pa)
+    const uint32_t z = (uint32_t)(p & 3);
+    const uint32_t head_nb = (uint32_t)((pa < pe_all ? pa : pe_all) - p);
+    const uint32_t tail_nb = (uint32_t)(pe_all - pe);
+    const bool has_head = z != 0, has_tail = tail_nb != 0 && pe >= pa;
+    constexpr uint32_t WB = 16 * WIN;
+    const uint64_t w0 = hw & ~(uint64_t)(WB - 1) & ~127ull;
+    const uint32_t o0 = (uint32_t)(w0 - rbase);
+    auto load_win = [&](u32x4 *buf, uint32_t off) {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) buf[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16 * q, 0, 0);
+    };
+    auto absorb = [&](const u32x4 *buf, uint64_t w) {
+        if (w >= pa && w + WB <= pe) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                c = T.word(c, buf[q].x); c = T.word(c, buf[q].y);
+                c = T.word(c, buf[q].z); c = T.word(c, buf[q].w);
+            }
+        } else if (w + WB > hw && w < pe_all) {
+#pragma unroll
+            for (int q = 0; q < 4 * WIN; q++) {
+                const uint32_t x = q % 4 == 0 ? buf[q / 4].x : q % 4 == 1 ? buf[q / 4].y : q % 4 == 2 ? buf[q / 4].z : buf[q / 4].w;
+                const uint64_t b = w + 4 * q;
+                if (b >= pa && b < pe) c = T.word(c, x);
+                else if (has_head && b == hw) c = T.partial(c, x >> (8 * z), head_nb);
+                else if (has_tail && b == pe) c = T.partial(c, x, tail_nb);
+            }
+        }
+    };
+    u32x4 A[WIN], Bf[WIN];
+    load_win(A, o0);
+    for (uint32_t k = 0; k < nwin_wave; k += 2) {
+        load_win(Bf, o0 + WB * (k + 1));
+        absorb(A, w0 + (uint64_t)WB * k);
+        if (k + 1 >= nwin_wave) break;
+        load_win(A, o0 + WB * (k + 2));
+        absorb(Bf, w0 + (uint64_t)WB * (k + 1));
+    }
+    return c;
+}
+
+// windows a block needs in crc_range_buf
+__device__ __forceinline__ uint32_t crc_buf_windows(uint64_t p, uint64_t len, uint32_t WB) {
+    if (len == 0) return 0;
+    const uint64_t w0 = (p & ~3ull) & ~(uint64_t)(WB - 1) & ~127ull;
+    return (uint32_t)((p + len - w0 + WB - 1) / WB);
+}
+
+template <class Tab>
+__device__ __forceinline__ uint32_t crc_range(const Tab &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
+    return crc_range_w<4, true>(T, c, p, len, end);
 }
 
 // FNV-1 (hash/fnv New32: multiply, then xor) over [p, p+len).

@@ -1,9 +1,266 @@
-// bhg_encode.hip -- placeholder (encode kernels land in the next milestone)
+// bhg_encode.hip -- batched BithashWriter.Add for gfx950.
+//
+// Pipeline (one launch sequence per batch, all on the caller's stream):
+//   k_enc_sizes   lane/record: key/value size checks (writer.go:258-265) and
+//                 record length L = 12 + (|ukey|+8) + |value'| (block2.go:73-105)
+//   scan          exclusive prefix of L -> record positions (bhg_scan.hip)
+//   k_enc_split   one workgroup: table split points -- after each successful
+//                 add, meta.Size >= TableMaxSize starts the next table
+//                 (bithash_writer.go:38,47-67); a 1024-ary search per table
+//   k_enc_pack    one WAVE per record: coalesced dword stores of
+//                 header | ukey | trailer | value into the output stream
+//   k_enc_crc     one LANE per record: masked CRC-32C of the packed record
+//                 (line-aligned windows, slice-by-4 LDS tables) + FNV-1 of
+//                 the user key (writer.go:246) + handle / table outputs
+// value' is the raw value (NoCompressor) or its golang/snappy encoding
+// (bhg_snappy_enc.hip) staged in ctx scratch.
+#include "bhg_device.h"
 #include "bhg_internal.h"
-extern "C" {
-int bhg_encode_batch(bhg_ctx *, const uint8_t *, const uint64_t *, const uint64_t *, const uint8_t *, const uint64_t *,
-                     uint32_t, int, const uint32_t *, uint32_t, uint32_t, uint64_t, uint8_t *, uint64_t,
-                     const bhg_encode_out *, void *) { return BHG_EINVAL; }
-int bhg_scan_tables(bhg_ctx *, const uint8_t *, const uint64_t *, uint32_t, int, bhg_handle *, uint64_t, uint64_t *,
-                    uint64_t *, void *) { return BHG_EINVAL; }
+
+namespace bhg {
+
+#define BHG_MAX_KEY_SIZE (33u << 10)          // writer.go:42
+#define BHG_MAX_VALUE_SIZE (256u << 20)       // writer.go:43
+
+struct EncArgs {
+    const uint8_t *keys;
+    const uint64_t *key_off;
+    const uint64_t *trailers;
+    const uint8_t *vals;          // value' bytes base (raw values or snappy scratch)
+    const uint64_t *vpos;         // value' start offset per record (into vals)
+    const uint64_t *vlen;         // value' length per record
+    uint32_t n;
+    const uint32_t *file_nums;
+    uint32_t max_tables;
+    uint32_t init_size;
+    uint64_t table_max;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *lens;               // scratch: L per record, then exclusive scan -> positions (n+1)
+    bhg_encode_out o;
+};
+
+__global__ __launch_bounds__(256) void k_enc_sizes(EncArgs a) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+        const uint64_t klen = a.key_off[i + 1] - a.key_off[i];
+        const uint64_t vl = a.vlen[i];
+        uint32_t st = BHG_ST_OK;
+        uint64_t L = 0;
+        if (klen + 8 > BHG_MAX_KEY_SIZE) st = BHG_ST_KEY_TOO_LARGE;
+        else if (vl > BHG_MAX_VALUE_SIZE) st = BHG_ST_VALUE_TOO_LARGE;
+        else L = 12 + klen + 8 + vl;
+        a.o.status[i] = st;
+        a.lens[i] = L;
+    }
+}
+
+// One workgroup of 1024 threads.  pos[0..n] = exclusive scan of L.
+// Table t starts at record s with start size S; it ends at the first record
+// e >= s with L_e > 0 and S + pos[e+1] - pos[s] >= table_max (the add that
+// reaches the limit stays in the table; a new, possibly empty, table follows).
+__device__ uint32_t first_geq(const uint64_t *pos, uint32_t lo, uint32_t hi, uint64_t T, uint32_t *s_best) {
+    // first e in [lo, hi) with pos[e+1] >= T, or hi; every thread returns the same value
+    while (lo < hi) {
+        const uint32_t span = hi - lo;
+        const uint32_t stepw = (span + 1023) / 1024;
+        __syncthreads();
+        if (threadIdx.x == 0) *s_best = hi;
+        __syncthreads();
+        const uint64_t e = (uint64_t)lo + (uint64_t)threadIdx.x * stepw;
+        if (e < hi && pos[e + 1] >= T) atomicMin(s_best, (uint32_t)e);
+        __syncthreads();
+        const uint32_t b = *s_best;
+        if (stepw == 1 || b == lo) return b;
+        if (b == hi) {
+            const uint32_t last = lo + ((span - 1) / stepw) * stepw;   // last (false) probe
+            lo = last + 1;
+        } else {
+            lo = b - stepw + 1;                                          // probe b - stepw was false
+            hi = b;
+        }
+    }
+    return hi;
+}
+
+__global__ __launch_bounds__(1024) void k_enc_split(EncArgs a) {
+    __shared__ uint32_t s_best;
+    const uint64_t *pos = a.lens;
+    const uint32_t n = a.n;
+    uint32_t s = 0, t = 0, fail = 0;
+    uint64_t S = a.init_size;
+    if (threadIdx.x == 0) a.o.table_start[0] = 0;
+    while (s < n) {
+        const uint64_t T = a.table_max > S ? pos[s] + (a.table_max - S) : pos[s];
+        uint32_t e = first_geq(pos, s, n, T, &s_best);
+        while (e < n && pos[e + 1] == pos[e]) e++;     // split check runs only after a successful add
+        if (e >= n) break;
+        if (t + 1 >= a.max_tables) { fail = 1; break; }
+        t++;
+        if (threadIdx.x == 0) a.o.table_start[t] = e + 1;
+        s = e + 1;
+        S = 0;
+    }
+    if (threadIdx.x == 0) {
+        a.o.summary[0] = pos[n];
+        a.o.summary[1] = fail ? 0 : t + 1;
+        a.o.summary[2] = 0;
+        a.o.summary[3] = fail;
+    }
+}
+
+// byte of the record stream at record offset o (o < 20 + klen): header / key / trailer
+__device__ __forceinline__ uint32_t prefix_byte(uint32_t o, uint32_t klen, uint32_t vl, uint32_t fn, uint64_t kp,
+                                                uint64_t trailer) {
+    if (o < 4) return ((klen + 8) >> (8 * o)) & 0xffu;
+    if (o < 8) return (vl >> (8 * (o - 4))) & 0xffu;
+    if (o < 12) return (fn >> (8 * (o - 8))) & 0xffu;
+    if (o < 12 + klen) return gld<uint8_t>(kp + (o - 12));
+    return (uint32_t)(trailer >> (8 * (o - 12 - klen))) & 0xffu;
+}
+
+// table index of record i: last t with table_start[t] <= i
+__device__ __forceinline__ uint32_t table_of(const uint32_t *ts, uint32_t nt, uint32_t i) {
+    uint32_t lo = 0, hi = nt;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ts[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+#define ENC_WAVES 4
+__global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * ENC_WAVES;
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    if (ntab == 0) return;  // split failed (max_tables too small)
+    const uint64_t vend = ~0ull;
+    for (uint32_t r = blockIdx.x * ENC_WAVES + (threadIdx.x >> 6); r < a.n; r += nw) {
+        if (a.o.status[r] != BHG_ST_OK) continue;
+        const uint64_t P = a.lens[r];
+        const uint32_t L = (uint32_t)(a.lens[r + 1] - P);
+        if (P + L > a.out_cap) continue;
+        const uint32_t klen = (uint32_t)(a.key_off[r + 1] - a.key_off[r]);
+        const uint32_t vl = (uint32_t)a.vlen[r];
+        const uint32_t t = table_of(a.o.table_start, ntab, r);
+        const uint32_t fn = a.file_nums[t];
+        const uint64_t kp = (uint64_t)a.keys + a.key_off[r];
+        const uint64_t trailer = a.trailers[r];
+        const uint64_t vp = (uint64_t)a.vals + a.vpos[r];
+        const uint64_t dst = (uint64_t)a.out + P;
+        const uint64_t d0 = dst & ~3ull;
+        const uint64_t dend = dst + L;
+        const uint32_t pre = 20 + klen;        // value starts at record offset pre
+        for (uint64_t q = d0 + 4ull * lane; q < dend; q += 256) {
+            const int64_t o0 = (int64_t)(q - dst);   // record offset of the dword's first byte (may be < 0)
+            uint32_t w = 0;
+            if (o0 >= (int64_t)pre) {
+                // whole dword inside the value: unaligned source read (2 aligned loads + alignbyte)
+                const uint64_t s = vp + (uint64_t)(o0 - pre);
+                const uint64_t sa = s & ~3ull;
+                const uint32_t lo = gld<uint32_t>(sa);
+                const uint32_t sh = (uint32_t)(s & 3);
+                const uint32_t hi = sh ? gld<uint32_t>(sa + 4) : 0u;
+                w = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+                (void)vend;
+                if (o0 + 4 <= (int64_t)L) {
+                    gst<uint32_t>(q, w);
+                    continue;
+                }
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int64_t o = o0 + b;
+                    if (o < 0 || o >= (int64_t)L) continue;
+                    uint32_t by;
+                    if (o < (int64_t)pre) by = prefix_byte((uint32_t)o, klen, vl, fn, kp, trailer);
+                    else by = gld<uint8_t>(vp + (uint64_t)(o - pre));
+                    w |= by << (8 * b);
+                }
+                if (o0 >= 0 && o0 + 4 <= (int64_t)L) {
+                    gst<uint32_t>(q, w);
+                    continue;
+                }
+            }
+            // partial dword at the record's first/last address: byte stores (neighbours own the rest)
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int64_t o = o0 + b;
+                if (o >= 0 && o < (int64_t)L) gst<uint8_t>(q + b, (uint8_t)(w >> (8 * b)));
+            }
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<R>::kWords];
+    Crc4Lds<R>::fill(T);
+    __syncthreads();
+    const Crc4Lds<R> crc(T);
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    const uint64_t out_end = (uint64_t)a.out + a.out_cap;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+        const uint64_t kp = (uint64_t)a.keys + a.key_off[i];
+        const uint32_t klen = (uint32_t)(a.key_off[i + 1] - a.key_off[i]);
+        a.o.fnv1[i] = fnv1_range(kp, klen, kp + klen);   // writer.go:246 (every Add, before add())
+        const uint32_t t = ntab ? table_of(a.o.table_start, ntab, i) : 0;
+        a.o.table[i] = t;
+        const uint64_t P = a.lens[i];
+        const uint32_t L = (uint32_t)(a.lens[i + 1] - P);
+        if (a.o.status[i] != BHG_ST_OK || ntab == 0 || P + L > a.out_cap) {
+            a.o.pos[i] = ~0ull;
+            a.o.bh_off[i] = 0;
+            a.o.bh_len[i] = 0;
+            a.o.crc[i] = 0;
+            continue;
+        }
+        a.o.pos[i] = P;
+        const uint64_t P0 = a.lens[a.o.table_start[t]];
+        a.o.bh_off[i] = (uint32_t)((t == 0 ? (uint64_t)a.init_size : 0ull) + (P - P0));
+        a.o.bh_len[i] = L;
+        a.o.crc[i] = crc_mask(~crc_range_a<8>(crc, 0xffffffffu, (uint64_t)a.out + P, L, out_end));
+    }
+}
+
+// value' = raw values: vpos = val_off, vlen = val_off[i+1]-val_off[i]
+__global__ __launch_bounds__(256) void k_enc_rawvals(const uint64_t *val_off, uint32_t n, uint64_t *vlen) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        vlen[i] = val_off[i + 1] - val_off[i];
+}
+
+hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
+    EncArgs a;
+    a.keys = E.keys; a.key_off = E.key_off; a.trailers = E.trailers;
+    a.vals = E.vbase; a.vpos = E.vpos; a.vlen = E.vlen;
+    a.n = E.n; a.file_nums = E.file_nums; a.max_tables = E.max_tables; a.init_size = E.init_size;
+    a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
+    const uint32_t g = lane_grid(L, E.n, 256);
+    hipLaunchKernelGGL(k_enc_sizes, dim3(g), dim3(256), 0, L.stream, a);
+    hipError_t e = launch_exclusive_scan_u64(L, E.lens, E.lens, E.n, E.scan_scratch);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_enc_split, dim3(1), dim3(1024), 0, L.stream, a);
+    uint32_t gp = (E.n + ENC_WAVES - 1) / ENC_WAVES;
+    const uint32_t capp = (uint32_t)L.num_cus * 8;
+    if (gp > capp) gp = capp;
+    if (gp == 0) gp = 1;
+    hipLaunchKernelGGL(k_enc_pack, dim3(gp), dim3(64 * ENC_WAVES), 0, L.stream, a);
+    uint32_t gc = (E.n + 511) / 512;
+    const uint32_t capc = (uint32_t)L.num_cus * 2;
+    if (gc > capc) gc = capc;
+    if (gc == 0) gc = 1;
+    hipLaunchKernelGGL(k_enc_crc<16>, dim3(gc), dim3(512), 0, L.stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen) {
+    hipLaunchKernelGGL(k_enc_rawvals, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, val_off, n, vlen);
+    return hipGetLastError();
+}
+
+}  // namespace bhg
+
+extern "C" int bhg_scan_tables(bhg_ctx *, const uint8_t *, const uint64_t *, uint32_t, int, bhg_handle *, uint64_t,
+                               uint64_t *, uint64_t *, void *) {
+    return BHG_EINVAL;  // implemented in a later milestone
 }

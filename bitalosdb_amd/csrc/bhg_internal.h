@@ -11,7 +11,8 @@ namespace bhg {
 struct Launch {
     hipStream_t stream;
     int num_cus;        // 256 on MI355X
-    int lane_wgs_per_cu;  // persistent workgroups per CU for the lane-per-block kernels
+    int lane_wgs_per_cu;  // override of resident workgroups per CU (0 = variant default)
+    int variant;          // lane-kernel variant (bhg_decode.hip kLaneVariants)
 };
 
 // persistent grid for lane-per-block kernels: enough workgroups to fill the
@@ -32,6 +33,28 @@ hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_l
                              uint32_t *out);
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
+
+// bhg_encode.hip
+struct EncodeLaunch {
+    const uint8_t *keys;
+    const uint64_t *key_off;
+    const uint64_t *trailers;
+    const uint8_t *vbase;      // value' bytes (raw values or snappy scratch)
+    const uint64_t *vpos;      // value' offsets into vbase
+    const uint64_t *vlen;      // value' lengths
+    uint32_t n;
+    const uint32_t *file_nums;
+    uint32_t max_tables;
+    uint32_t init_size;
+    uint64_t table_max;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *lens;            // scratch n+1
+    void *scan_scratch;
+    bhg_encode_out o;
+};
+hipError_t launch_encode(const Launch &L, const EncodeLaunch &E);
+hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen);
 
 // bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
 // scratch must hold scan_scratch_bytes(n).

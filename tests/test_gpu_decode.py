@@ -71,7 +71,7 @@ def test_mixed_sizes_and_alignment(codec, gap):
     rng = random.Random(gap)
     specs = []
     for i in range(1500):
-        kl = rng.choice([0, 1, 5, 7, 8, 16, 31, 32, 33, 100])
+        kl = rng.choice([0, 1, 5, 7, 8, 16, 31, 32, 33, 35, 36, 37, 39, 40, 41, 48, 100])
         vl = rng.choice([1, 2, 3, 4, 5, 63, 64, 65, 300, 1024, 1025, 4096, 9000])
         specs.append((rand_bytes(rng, kl), rand_bytes(rng, vl), rng.randrange(1 << 32)))
     src, h = make_records(rng, specs, gap_max=gap)
@@ -272,3 +272,19 @@ def _full_size(codec, synth, handles_tensor, n):
     assert_desc_equal(got, exp)
     assert (got["status"] == 0).all()
     assert (got["trailer"] >> 8 == np.arange(1, n + 1)).all()
+
+
+@pytest.mark.parametrize("variant", [v for v in range(44) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
+def test_lane_kernel_variants(variant, monkeypatch):
+    """Every CRC-table flavour of k_decode_lane is bit-exact (slice-by-1/4, R=4..32)."""
+    from bitalosdb_amd.codec import BithashCodec
+    monkeypatch.setenv("BHG_DECODE_VARIANT", str(variant))
+    c = BithashCodec(0)
+    rng = random.Random(100 + variant)
+    specs = [(rand_bytes(rng, rng.choice([0, 7, 32])), rand_bytes(rng, rng.choice([1, 3, 64, 1024, 2047])), 5)
+             for _ in range(2000)]
+    src, h = make_records(rng, specs, gap_max=3)
+    got, _, _ = c.decode(src, h)
+    exp, _, _ = O.decode_batch(src, h)
+    assert_desc_equal(got, exp)
+    c.close()
