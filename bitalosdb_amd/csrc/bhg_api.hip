@@ -105,7 +105,7 @@ bhg_ctx *bhg_create(int device, int flags) {
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     c->lane_wgs_per_cu = 0;
-    c->variant = 1;
+    c->variant = 28;  // k_decode_lane: slice-4 x16, 128 B line-aligned prefetched windows (bhg_decode.hip)
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
     if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
     c->err[0] = 0;
@@ -313,19 +313,38 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
         set_err(c, "null buffer");
         return BHG_EINVAL;
     }
-    if (codec == BHG_CODEC_SNAPPY) { set_err(c, "snappy encode: not built in this version"); return BHG_EINVAL; }
     std::lock_guard<std::mutex> g(c->mu);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t lens_b = al(((size_t)n + 1) * 8), vlen_b = al((size_t)n * 8), scan_b = al(bhg::scan_scratch_bytes(n));
-    if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, lens_b + vlen_b + scan_b)) return r;
+    const size_t lens_b = al(((size_t)n + 1) * 8), vlen_b = al(((size_t)n + 1) * 8), scan_b = al(bhg::scan_scratch_bytes(n));
+    size_t snap_b = 0, soff_b = 0, gt_b = 0;
+    uint64_t vbytes = 0;
+    if (codec == BHG_CODEC_SNAPPY) {
+        // bound of the compressed scratch: sum MaxEncodedLen <= 32 n + V + V/6 (needs V = val_off[n])
+        HIP_TRY(c, hipMemcpyAsync(&vbytes, val_off + n, 8, hipMemcpyDeviceToHost, L.stream));
+        HIP_TRY(c, hipStreamSynchronize(L.stream));
+        snap_b = al((size_t)(32ull * n + vbytes + vbytes / 6 + 64));
+        soff_b = al(((size_t)n + 1) * 8);
+        gt_b = al((size_t)bhg::snappy_enc_grid(L, n) * 16384 * 2);
+    }
+    if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b)) return r;
     uint8_t *sp = reinterpret_cast<uint8_t *>(c->scratch);
     bhg::EncodeLaunch E;
     E.lens = reinterpret_cast<uint64_t *>(sp);
     uint64_t *vlen = reinterpret_cast<uint64_t *>(sp + lens_b);
     E.scan_scratch = sp + lens_b + vlen_b;
-    HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
+    if (codec == BHG_CODEC_SNAPPY) {
+        uint8_t *snap = sp + lens_b + vlen_b + scan_b;
+        uint64_t *soff = reinterpret_cast<uint64_t *>(snap + snap_b);
+        uint16_t *gt = reinterpret_cast<uint16_t *>(snap + snap_b + soff_b);
+        HIP_TRY(c, bhg::launch_snappy_maxlen(L, val_off, n, soff));
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, soff, soff, n, E.scan_scratch));
+        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, soff, vlen, gt));
+        E.vbase = snap; E.vpos = soff; E.vlen = vlen;
+    } else {
+        HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
+        E.vbase = vals; E.vpos = val_off; E.vlen = vlen;
+    }
     E.keys = keys; E.key_off = key_off; E.trailers = trailers;
-    E.vbase = vals; E.vpos = val_off; E.vlen = vlen;
     E.n = n; E.file_nums = file_nums; E.max_tables = max_tables; E.init_size = init_size; E.table_max = table_max;
     E.out = out; E.out_cap = out_cap; E.o = *o;
     HIP_TRY(c, bhg::launch_encode(L, E));

@@ -577,7 +577,8 @@ __global__ __launch_bounds__(WG) void k_decode_lanebuf(const uint8_t *__restrict
                 const uint32_t nrec = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)span;
                 const __amdgpu_buffer_rsrc_t rsrc =
                     __builtin_amdgcn_make_buffer_rsrc((void *)rbase, (short)0, (int)nrec, 0x00020000);
-                uint32_t cc = crc_range_buf<WIN>(crc, 0xffffffffu, inb ? p : rbase, inb ? L : 0, rsrc, rbase, nwin);
+                uint32_t cc = crc_range_buf<WIN>(crc, 0xffffffffu, inb ? p : rbase, inb ? L : 0, rsrc, rbase, nwin,
+                                                  rbase + nrec);
                 c = cc;
             } else if (inb) {
                 c = crc_range_pp<WIN>(crc, 0xffffffffu, p, L, end);
@@ -1010,7 +1011,7 @@ static void launch_lane_mode(const Launch &L, int variant, const uint8_t *src, u
 hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes) {
     int variant = L.variant;
-    if (variant < 0 || variant >= kNumLaneVariants) variant = 1;
+    if (variant < 0 || variant >= kNumLaneVariants) variant = 28;
     if (codec == BHG_CODEC_NONE)
         launch_lane_mode<MODE_NONE>(L, variant, src, src_len, h, n, expected_crc, out, sizes);
     else

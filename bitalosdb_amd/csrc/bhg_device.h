@@ -403,7 +403,8 @@ __device__ __forceinline__ uint32_t crc_range_pp(const Tab &T, uint32_t c, uint6
 // same windows.  `rel` = absolute address - descriptor base (< 2^32).
 template <int WIN, class Tab>
 __device__ __forceinline__ uint32_t crc_range_buf(const Tab &T, uint32_t c, uint64_t p, uint64_t len,
-                                                  __amdgpu_buffer_rsrc_t rsrc, uint64_t rbase, uint32_t nwin_wave) {
+                                                  __amdgpu_buffer_rsrc_t rsrc, uint64_t rbase, uint32_t nwin_wave,
+                                                  uint64_t rend) {
     const uint64_t pe_all = p + len;
     const uint64_t pa = (p + 3) & ~3ull;
     const uint64_t pe = pe_all & ~3ull;
@@ -429,8 +430,10 @@ __device__ __forceinline__ uint32_t crc_range_buf(const Tab &T, uint32_t c, uint
         } else if (w + WB > hw && w < pe_all) {
 #pragma unroll
             for (int q = 0; q < 4 * WIN; q++) {
-                const uint32_t x = q % 4 == 0 ? buf[q / 4].x : q % 4 == 1 ? buf[q / 4].y : q % 4 == 2 ? buf[q / 4].z : buf[q / 4].w;
+                uint32_t x = q % 4 == 0 ? buf[q / 4].x : q % 4 == 1 ? buf[q / 4].y : q % 4 == 2 ? buf[q / 4].z : buf[q / 4].w;
                 const uint64_t b = w + 4 * q;
+                // a dwordx4 that straddles the descriptor end comes back all-zero: re-read its words
+                if (w + 16 * (q / 4) + 16 > rend && b < rend) x = ld32_safe(b, rend);
                 if (b >= pa && b < pe) c = T.word(c, x);
                 else if (has_head && b == hw) c = T.partial(c, x >> (8 * z), head_nb);
                 else if (has_tail && b == pe) c = T.partial(c, x, tail_nb);

@@ -56,6 +56,12 @@ struct EncodeLaunch {
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E);
 hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen);
 
+// bhg_snappy_enc.hip
+hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *out);
+uint32_t snappy_enc_grid(const Launch &L, uint32_t n);
+hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
+                             uint8_t *scratch, const uint64_t *soff, uint64_t *clen, uint16_t *gtables);
+
 // bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
 // scratch must hold scan_scratch_bytes(n).
 size_t scan_scratch_bytes(uint64_t n);
