@@ -21,6 +21,9 @@ import time
 import numpy as np
 import torch
 
+DESC_DT = np.dtype([("key_off", "<u4"), ("key_len", "<u4"), ("val_off", "<u4"), ("val_len", "<u4"),
+                    ("trailer", "<u8"), ("file_num", "<u4"), ("fnv1", "<u4"), ("crc", "<u4"), ("status", "<u4")])
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -38,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"],
+                    help="c2: uncompressed decode (BASELINE metric); c3: snappy decode; c4: encode")
     return ap.parse_args()
 
 
@@ -89,6 +94,10 @@ def main():
 
 
 def run(a, world, rank, local, dev, codec):
+    if a.config == "c3":
+        return run_c3(a, world, rank, local, dev, codec)
+    if a.config == "c4":
+        return run_c4(a, world, rank, local, dev, codec)
     import torch.distributed as dist
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import handles_tensor
@@ -134,16 +143,8 @@ def run(a, world, rank, local, dev, codec):
                   ("status", "<u4")]))
     ok_blocks = int((d["status"] == 0).sum())
     digest = int(np.bitwise_xor.reduce(d["crc"].astype(np.uint64) * np.uint64(0x9E3779B1) ^ d["fnv1"]))
-    stats = torch.tensor([elapsed, float(ok_blocks), float(n)], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = stats[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = stats[1:].clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx.item())
-        ok_total, n_total = float(sm[0].item()), float(sm[1].item())
-    else:
-        ok_total, n_total = float(ok_blocks), float(n)
+    from bitalosdb_amd import shard
+    elapsed, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok_blocks, n, digest & (2 ** 64 - 1), dev)
 
     total_blocks = n_total * a.steps
     value = total_blocks * L / elapsed / 2 ** 30
@@ -171,7 +172,7 @@ def run(a, world, rank, local, dev, codec):
                      "kernel": "k_decode_lane<MODE_NONE,4,16,512,8,2>", "kernel_avg_ms": round(avg_kern_ms, 4),
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK},
         "status_ok_blocks": int(ok_total),
-        "digest_rank0": "%016x" % (digest & (2 ** 64 - 1)),
+        "digest_all_ranks": "%016x" % digest_all,
     }
 
     if rank == 0 and world == 1 and not a.no_e2e:
@@ -216,6 +217,166 @@ def run(a, world, rank, local, dev, codec):
 
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def _pack_values(vals_t):
+    """[n, L] uint8 device tensor -> (flat bytes, u64 offsets[n+1]) device tensors."""
+    n, L = vals_t.shape
+    off = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=vals_t.device)
+    return vals_t.reshape(-1).contiguous(), off
+
+
+def _encode_inputs(n, val_lens, dev, seed):
+    """Keys/trailers/values for n pairs (values from the compressible generator)."""
+    from bitalosdb_amd import synth
+    keys = synth.keys_gpu(n, device=dev, seed=seed)
+    key_off = torch.arange(0, (n + 1) * 32, 32, dtype=torch.int64, device=dev)
+    tr = (torch.arange(1, n + 1, dtype=torch.int64, device=dev) << 8) | 1
+    maxlen = int(val_lens.max().item())
+    # ragged values: value i is the first val_lens[i] bytes of row i (row-major masked_select = concatenation)
+    val_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    val_off[1:] = torch.cumsum(val_lens, 0)
+    parts = []
+    chunk = 1 << 16
+    cols = torch.arange(maxlen, device=dev)
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        raw = synth.compressible_values_gpu(m, maxlen, device=dev, seed=seed + c0)
+        parts.append(torch.masked_select(raw, cols.unsqueeze(0) < val_lens[c0:c0 + m].unsqueeze(1)))
+    vals = torch.cat(parts)
+    return keys.reshape(-1).contiguous(), key_off, tr, vals, val_off
+
+
+def _encode_tables(codec, n, val_lens, dev, seed, compressor):
+    """Encode n pairs into bithash tables on the GPU; returns (src, handles, meta, raw_bytes)."""
+    from bitalosdb_amd.codec import EncodeBuffers, HANDLE_DT
+    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, seed)
+    cap = int(n * 64 + vals.numel() * 7 // 6 + 64)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    maxt = 4096
+    fns = torch.arange(1, maxt + 1, dtype=torch.int32, device=dev)
+    bufs = EncodeBuffers(n, maxt, dev)
+    codec.encode_batch(keys, key_off, tr, vals, val_off, n, compressor, fns, maxt, 0, 128 << 20, out, bufs)
+    codec.sync()
+    pos = bufs.pos.cpu().numpy().view(np.uint64)
+    ln = bufs.bh_len.cpu().numpy().view(np.uint32)
+    h = np.zeros(n, dtype=HANDLE_DT)
+    h["offset"] = pos
+    h["length"] = ln
+    total = int(bufs.summary[0].item())
+    return out[:total], h, dict(src_bytes=total, ntables=int(bufs.summary[1].item())), (keys, key_off, tr, vals, val_off, bufs)
+
+
+def _timed(a, dev, fn):
+    for _ in range(a.warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        starts[i].record()
+        fn()
+        ends[i].record()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return el, float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+
+def run_c3(a, world, rank, local, dev, codec):
+    """BASELINE configs[2]: 1M snappy blocks, full CRC + decompress + decode, 32 B / 1 KiB."""
+    n = a.blocks
+    val_lens = torch.full((n,), 1024, dtype=torch.int64, device=dev)
+    src, h, meta, _ = _encode_tables(codec, n, val_lens, dev, synth_seed(rank), 1)
+    from bitalosdb_amd.codec import handles_tensor
+    h_t = handles_tensor(h, dev)
+    desc = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    voff = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev)
+    vals = torch.empty(n * 1024 + 64, dtype=torch.uint8, device=dev)
+    step = lambda: codec.decode_batch(src, src.numel(), h_t, n, 1, out_desc=desc, out_vals=vals, out_val_off=voff)
+    el, kms = _timed(a, dev, step)
+    d = desc.cpu().numpy().view(DESC_DT)
+    disk = float(h["length"].astype(np.float64).sum())
+    out = {"metric": "GiB/s bithash blocks decoded (device-resident), snappy, 32B key / 1KB value, 1 GPU",
+           "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (GPU-encoded snappy tables)",
+           "config": {"workload": "BASELINE configs[2]: 1M snappy blocks, CRC + decompress + decode",
+                      "blocks_per_gpu": n, "mean_record_bytes": round(disk / n, 1),
+                      "decoded_GiBps": round(n * 1024 * a.steps / el / 2 ** 30, 3)},
+           "status_ok_blocks": int((d["status"] == 0).sum())}
+    if rank == 0 and world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+        host = src.cpu().numpy()
+        exp, ev, eo = O.decode_batch(host, h, codec=1, nthreads=min(16, os.cpu_count() or 1))
+        got_v = vals.cpu().numpy()
+        par = all(np.array_equal(exp[f], d[f]) for f in d.dtype.names) and \
+            got_v[:int(eo[-1])].tobytes() == ev[:int(eo[-1])].tobytes()
+        thr = min(16, os.cpu_count() or 1)
+        t = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t < a.cpu_seconds:
+            O.decode_batch(host, h, codec=1, nthreads=thr, out_val_off=eo)
+            reps += 1
+        cs = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": round(reps * disk / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": thr,
+                               "kind": "port", "sample": "%d passes over the same %d blocks (%s)" % (reps, n, cpu_info())}
+        out["parity_vs_restatement"] = "bit-exact" if par else "MISMATCH"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def run_c4(a, world, rank, local, dev, codec):
+    """BASELINE configs[3]: encode 1M pairs, values U[64, 4096] B -> record-pack + snappy + CRC."""
+    from bitalosdb_amd.codec import EncodeBuffers
+    n = a.blocks
+    g = torch.Generator(device=dev)
+    g.manual_seed(synth_seed(rank) + 7)
+    val_lens = torch.randint(64, 4097, (n,), generator=g, device=dev, dtype=torch.int64)
+    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, synth_seed(rank))
+    cap = int(n * 64 + vals.numel() * 7 // 6 + 64)
+    out_t = torch.empty(cap, dtype=torch.uint8, device=dev)
+    maxt = 4096
+    fns = torch.arange(1, maxt + 1, dtype=torch.int32, device=dev)
+    bufs = EncodeBuffers(n, maxt, dev)
+    step = lambda: codec.encode_batch(keys, key_off, tr, vals, val_off, n, 1, fns, maxt, 0, 128 << 20, out_t, bufs)
+    el, kms = _timed(a, dev, step)
+    raw = float(vals.numel() + n * 32)
+    total = int(bufs.summary[0].item())
+    res = {"metric": "GiB/s KV input encoded (record-pack + snappy + CRC), values 64B-4KB, 1 GPU",
+           "value": round(raw * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic compressible values",
+           "config": {"workload": "BASELINE configs[3]: 1M KV pairs -> record-pack + compress + CRC",
+                      "pairs_per_gpu": n, "input_bytes": int(raw), "output_bytes": total,
+                      "tables": int(bufs.summary[1].item())}}
+    if rank == 0 and world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+        # bounded sample: the first 20k pairs, single thread (the restated writer is serial)
+        m = min(n, 20000)
+        vo = val_off.cpu().numpy()
+        vb = vals.cpu().numpy()
+        kb = keys.cpu().numpy()
+        ks = [kb[32 * i:32 * i + 32].tobytes() for i in range(m)]
+        vs = [vb[vo[i]:vo[i + 1]].tobytes() for i in range(m)]
+        trs = tr[:m].cpu().numpy()
+        t = time.perf_counter()
+        exp = O.encode_batch(ks, trs, vs, codec=1, file_nums=list(range(1, 100)))
+        cs = time.perf_counter() - t
+        got_out = out_t.cpu().numpy()
+        par = got_out[:len(exp["out"])].tobytes() == exp["out"].tobytes()
+        res["cpu_baseline"] = {"value": round(float(sum(len(v) for v in vs) + 32 * m) / cs / 2 ** 30, 3),
+                               "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": "first %d pairs, restated BithashWriter.Add + golang/snappy Encode, 1 thread (%s)"
+                                         % (m, cpu_info())}
+        res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def synth_seed(rank):
+    from bitalosdb_amd import synth
+    return synth.SEED + rank
 
 
 if __name__ == "__main__":

@@ -1,0 +1,36 @@
+"""Table-file sharding over the GPUs of one node.
+
+Bithash tables (`<fileNum>.bht`) are immutable and self-contained, so decode
+shards by table file with no data-path exchange: table t is owned by rank
+t mod world (round-robin).  The only collective is a final reduction of
+counters / timing over RCCL (backend "nccl") -- or gloo in the CPU tests.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def table_owner(table_index, world):
+    return table_index % world
+
+
+def owned_tables(ntables, world, rank):
+    return [t for t in range(ntables) if table_owner(t, world) == rank]
+
+
+def shard_handles(handles, table_of_handle, world, rank):
+    """Handles (HANDLE_DT array) whose table index belongs to `rank`."""
+    mask = (np.asarray(table_of_handle) % world) == rank
+    return handles[mask]
+
+
+def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
+    """MAX of elapsed, SUM of block counts, XOR-fold of per-rank digests (as sum of
+    64-bit halves mod 2^32 pairs); returns python values.  Runs outside the timed region."""
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    c = torch.tensor([ok_blocks, n_blocks, digest & 0xFFFFFFFF, digest >> 32], dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    c = c.cpu().tolist()
+    return float(t.item()), int(c[0]), int(c[1]), (int(c[2]) & 0xFFFFFFFF) | ((int(c[3]) & 0xFFFFFFFF) << 32)

@@ -89,3 +89,32 @@ def compressible_values(rng, n_vals, val_len, dict_size=4096, fresh=0.2):
                 row[pos:pos + m] = d[st:st + m]
             pos += ln
     return out
+
+
+def compressible_values_gpu(n, val_len, device="cuda", seed=SEED, words=8, word_len=16, fresh_frac=0.25):
+    """[n, val_len] uint8 values on the GPU: 16-byte chunks drawn from a per-value
+    set of `words` random words, a quarter of the chunks fresh random bytes --
+    snappy sees intra-value repetition (about 2:1 for 1 KiB values)."""
+    device = torch.device(device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    nch = -(-val_len // word_len)
+    out = torch.empty((n, nch * word_len), dtype=torch.uint8, device=device)
+    chunk = 1 << 15
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        w = torch.randint(0, 256, (m, words, word_len), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+        pick = torch.randint(0, words, (m, nch), generator=g, device=device)
+        fresh = torch.rand((m, nch), generator=g, device=device) < fresh_frac
+        rnd = torch.randint(0, 256, (m, nch, word_len), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+        sel = torch.gather(w, 1, pick.unsqueeze(-1).expand(m, nch, word_len))
+        sel = torch.where(fresh.unsqueeze(-1), rnd, sel)
+        out[c0:c0 + m] = sel.reshape(m, nch * word_len)
+    return out[:, :val_len]
+
+
+def keys_gpu(n, key_len=32, device="cuda", seed=SEED + 1):
+    device = torch.device(device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return _rand_alpha(g, (n, key_len), device, _alpha(device))

@@ -30,6 +30,22 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv \
         -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu --no-e2e > $OUT/prof.log 2>&1 || exit $?
       find $OUT/prof -name "*stats*" | head ;;
+    c3)
+      timeout -k 10 600 python bench.py --config c3 --steps 10 --warmup 2 --cpu-seconds 8 > $OUT/bench_c3.log 2>&1 || exit $?
+      cat $OUT/bench_c3.log ;;
+    c4)
+      timeout -k 10 600 python bench.py --config c4 --steps 5 --warmup 1 > $OUT/bench_c4.log 2>&1 || exit $?
+      cat $OUT/bench_c4.log ;;
+    profc3)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/profc3 -o run --output-format csv \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --config c3 --steps 5 --warmup 1 --no-cpu > $OUT/profc3.log 2>&1 || exit $?
+      find $OUT/profc3 -name "*stats*" | head ;;
+    profc4)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/profc4 -o run --output-format csv \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --config c4 --steps 3 --warmup 1 --no-cpu > $OUT/profc4.log 2>&1 || exit $?
+      find $OUT/profc4 -name "*stats*" | head ;;
     pmc)
       export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/$OUT/pmc1 -o run --output-format csv \

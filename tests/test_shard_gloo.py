@@ -1,0 +1,59 @@
+"""N>1 path on CPU: world_size-2 gloo run of the table sharding + stats
+reduction that bench.py uses over RCCL on the GPU node."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from bitalosdb_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ntables = 9
+    mine = shard.owned_tables(ntables, world, rank)
+    # 100 blocks per table; each rank "decodes" its tables
+    handles = np.zeros(ntables * 100, dtype=[("offset", "<u8"), ("length", "<u4"), ("pad", "<u4")])
+    tab = np.repeat(np.arange(ntables), 100)
+    sub = shard.shard_handles(handles, tab, world, rank)
+    el, ok, n, dg = shard.reduce_stats(0.5 + rank, len(sub), len(sub), 1000 + rank, torch.device("cpu"))
+    q.put((rank, mine, len(sub), el, ok, n, dg))
+    dist.destroy_process_group()
+
+
+def test_world2_gloo_sharding():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    (r0, m0, s0, el0, ok0, n0, d0), (r1, m1, s1, el1, ok1, n1, d1) = res
+    assert m0 == [0, 2, 4, 6, 8] and m1 == [1, 3, 5, 7]
+    assert s0 == 500 and s1 == 400
+    assert el0 == el1 == 1.5                      # max over ranks
+    assert ok0 == ok1 == n0 == n1 == 900          # sum over ranks
+    assert d0 == d1 == 2001
+
+
+def test_single_process_reduce():
+    import torch
+    el, ok, n, dg = shard.reduce_stats(1.25, 7, 8, (5 << 32) | 9, torch.device("cpu"))
+    assert (el, ok, n, dg) == (1.25, 7, 8, (5 << 32) | 9)
