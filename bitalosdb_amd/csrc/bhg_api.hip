@@ -20,6 +20,7 @@ struct bhg_ctx {
     int num_cus;
     int lane_wgs_per_cu;
     int variant;
+    int snappy_variant;
     char err[512];
     std::mutex mu;          // guards scratch growth and the host-path buffers
     void *scratch = nullptr;
@@ -56,6 +57,7 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     L.num_cus = c->num_cus;
     L.lane_wgs_per_cu = c->lane_wgs_per_cu;
     L.variant = c->variant;
+    L.snappy_variant = c->snappy_variant;
     return L;
 }
 
@@ -108,6 +110,8 @@ bhg_ctx *bhg_create(int device, int flags) {
     c->variant = 28;  // k_decode_lane: slice-4 x16, 128 B line-aligned prefetched windows (bhg_decode.hip)
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
     if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
+    c->snappy_variant = 0;
+    if (const char *s = getenv("BHG_SNAPPY_VARIANT")) c->snappy_variant = atoi(s);
     c->err[0] = 0;
     // blocking stream: orders against the legacy NULL stream, so callers that
     // stage buffers on the default stream need no extra event

@@ -416,6 +416,129 @@ __global__ __launch_bounds__(64 * SNAPPY_WAVES_PER_WG) void k_snappy_wave(
 }
 
 // ---------------------------------------------------------------------------
+// golang/snappy v0.0.4 decode, one LANE per block (decode_other.go `decode`).
+// gfx950 runs unaligned global dword/dwordx4 accesses natively, so a lane
+// moves literals and non-overlapping copies 16 B at a time straight from the
+// record (input) / its own output (copy source) into its output slot; the
+// last chunk may overshoot into bytes that later elements overwrite (never
+// past the block's dlen).  Overlapping copies go 4 B (offset >= 4) or 1 B
+// at a time.  ~64 x 32 x 256 blocks are in flight chip-wide, which hides
+// the per-element load latency that a wave-per-block walk exposes.
+// A lane's loads of its own earlier stores are ordered by the memory
+// pipeline (same wave, same address).
+// ---------------------------------------------------------------------------
+typedef uint32_t u32a1 __attribute__((aligned(1)));
+typedef uint64_t u64a1 __attribute__((aligned(1)));
+typedef u32x4 u32x4a1 __attribute__((aligned(1)));
+
+__device__ __forceinline__ uint64_t ldu64_g(uint64_t a, uint64_t end) {
+    if (a + 8 <= end) return gld<u64a1>(a);
+    uint64_t x = 0;
+    for (uint32_t b = 0; b < 8; b++)
+        if (a + b < end) x |= (uint64_t)gld<uint8_t>(a + b) << (8 * b);
+    return x;
+}
+
+// returns true on success; cp/dst absolute addresses
+__device__ __forceinline__ bool snappy_lane_decode(uint64_t cp, uint32_t slen, uint64_t dst, uint32_t dlen,
+                                                   uint64_t end) {
+    uint32_t s = 0, d = 0;
+    while (s < slen) {
+        const uint64_t t8 = ldu64_g(cp + s, end);
+        const uint32_t tag = (uint32_t)t8 & 0xffu;
+        uint32_t length, offset;
+        if ((tag & 3) == 0) {
+            uint32_t x = tag >> 2;
+            uint64_t l64;
+            if (x < 60) {
+                s += 1;
+                l64 = (uint64_t)x + 1;
+            } else {
+                const uint32_t nb = x - 59;
+                if ((uint64_t)s + 1 + nb > slen) return false;
+                s += 1 + nb;
+                x = (uint32_t)(t8 >> 8) & (nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u));
+                l64 = (uint64_t)x + 1;
+            }
+            if (l64 > (uint64_t)(dlen - d) || l64 > (uint64_t)(slen - s)) return false;
+            length = (uint32_t)l64;
+            uint32_t k = 0;
+            for (; k + 16 <= length || (k < length && d + k + 16 <= dlen && cp + s + k + 16 <= end); k += 16)
+                gst<u32x4a1>(dst + d + k, gld<u32x4a1>(cp + s + k));
+            for (; k < length; k++) gst<uint8_t>(dst + d + k, gld<uint8_t>(cp + s + k));
+            d += length;
+            s += length;
+            continue;
+        } else if ((tag & 3) == 1) {
+            if ((uint64_t)s + 2 > slen) return false;
+            s += 2;
+            length = 4 + ((tag >> 2) & 7);
+            offset = ((tag & 0xe0) << 3) | ((uint32_t)(t8 >> 8) & 0xffu);
+        } else if ((tag & 3) == 2) {
+            if ((uint64_t)s + 3 > slen) return false;
+            s += 3;
+            length = 1 + (tag >> 2);
+            offset = (uint32_t)(t8 >> 8) & 0xffffu;
+        } else {
+            if ((uint64_t)s + 5 > slen) return false;
+            s += 5;
+            length = 1 + (tag >> 2);
+            offset = (uint32_t)(t8 >> 8);
+        }
+        if (offset == 0 || d < offset || length > dlen - d) return false;
+        const uint64_t o = dst + d, from = o - offset;
+        if (offset >= 16) {
+            uint32_t k = 0;
+            for (; k + 16 <= length || (k < length && d + k + 16 <= dlen); k += 16)
+                gst<u32x4a1>(o + k, gld<u32x4a1>(from + k));
+            for (; k < length; k++) gst<uint8_t>(o + k, gld<uint8_t>(from + k));
+        } else if (offset >= 4) {
+            uint32_t k = 0;
+            for (; k + 4 <= length || (k < length && d + k + 4 <= dlen); k += 4)
+                gst<u32a1>(o + k, gld<u32a1>(from + k));
+            for (; k < length; k++) gst<uint8_t>(o + k, gld<uint8_t>(from + k));
+        } else {
+            for (uint32_t k = 0; k < length; k++) gst<uint8_t>(o + k, gld<uint8_t>(from + k));
+        }
+        d += length;
+    }
+    return d == dlen;
+}
+
+__global__ __launch_bounds__(256) void k_snappy_lane(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                     const bhg_handle *__restrict__ handles, uint32_t n,
+                                                     bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
+                                                     uint64_t out_cap, const uint64_t *__restrict__ val_off) {
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
+        const uint32_t status = dw[9];
+        if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
+        const uint32_t cpos = dw[2], dlen = dw[3];
+        const bhg_handle h = handles[i];
+        const uint64_t rec = base + h.offset;
+        const uint32_t clen = h.length - cpos;
+        const uint64_t o0 = val_off[i], o1 = val_off[i + 1];
+        uint32_t fin = status;
+        if (o1 > out_cap || o1 - o0 < dlen) {
+            fin = BHG_ST_SNAPPY_TOO_LARGE;
+        } else {
+            const uint64_t cp = rec + cpos;
+            uint32_t hdr = 0;
+            for (;;) {  // varint already validated by the lane pass
+                const uint32_t b = gld<uint8_t>(cp + hdr);
+                hdr++;
+                if (b < 0x80) break;
+            }
+            if (!snappy_lane_decode(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end)) fin = BHG_ST_SNAPPY_CORRUPT;
+        }
+        dw[2] = 0;
+        dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? dlen : 0u;
+        dw[9] = fin;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // batched primitives
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_crc_ranges(const uint8_t *__restrict__ src, uint64_t src_len,
@@ -1021,6 +1144,15 @@ hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_
 
 hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
+    if (L.snappy_variant == 0) {
+        uint32_t grid = (n + 255) / 256;
+        const uint32_t cap = (uint32_t)L.num_cus * 8;
+        if (grid > cap) grid = cap;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL(k_snappy_lane, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
+                           out_cap, val_off);
+        return hipGetLastError();
+    }
     uint32_t grid = (n + SNAPPY_WAVES_PER_WG - 1) / SNAPPY_WAVES_PER_WG;
     const uint32_t cap = (uint32_t)L.num_cus * 16;
     if (grid > cap) grid = cap;

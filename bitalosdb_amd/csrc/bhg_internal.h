@@ -13,6 +13,7 @@ struct Launch {
     int num_cus;        // 256 on MI355X
     int lane_wgs_per_cu;  // override of resident workgroups per CU (0 = variant default)
     int variant;          // lane-kernel variant (bhg_decode.hip kLaneVariants)
+    int snappy_variant;   // 0: lane-per-block snappy decode, 1: wave-per-block
 };
 
 // persistent grid for lane-per-block kernels: enough workgroups to fill the

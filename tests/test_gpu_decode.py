@@ -288,3 +288,25 @@ def test_lane_kernel_variants(variant, monkeypatch):
     exp, _, _ = O.decode_batch(src, h)
     assert_desc_equal(got, exp)
     c.close()
+
+
+@pytest.mark.parametrize("sv", [0, 1])
+def test_snappy_kernel_variants(sv, monkeypatch):
+    """lane-per-block and wave-per-block snappy decoders are both bit-exact."""
+    from bitalosdb_amd.codec import BithashCodec
+    monkeypatch.setenv("BHG_SNAPPY_VARIANT", str(sv))
+    c = BithashCodec(0)
+    rng = random.Random(300 + sv)
+    specs = []
+    for i in range(1500):
+        vl = rng.choice([1, 3, 15, 16, 17, 31, 64, 100, 1024, 1024, 3000, 5000, 70000 if i % 500 == 0 else 2000])
+        kind = i % 4
+        v = compressible(rng, vl) if kind == 0 else (b"abc" * vl)[:vl] if kind == 1 else \
+            (b"a" * vl) if kind == 2 else rand_bytes(rng, vl)
+        specs.append((rand_bytes(rng, 32), v, 2))
+    src, h = make_records(rng, specs, gap_max=5, codec=1)
+    got, gv, go = c.decode(src, h, compressor=1)
+    exp, ev, eo = O.decode_batch(src, h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(go, eo) and gv.tobytes() == ev[:int(eo[-1])].tobytes()
+    c.close()
