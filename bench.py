@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"],
-                    help="c2: uncompressed decode (BASELINE metric); c3: snappy decode; c4: encode")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "scan", "scanmix"],
+                    help="c2: uncompressed decode (BASELINE metric); c3: snappy decode; c4: encode; "
+                         "scan/scanmix: table data-region scan over uniform / mixed-length tables")
     return ap.parse_args()
 
 
@@ -98,6 +99,8 @@ def run(a, world, rank, local, dev, codec):
         return run_c3(a, world, rank, local, dev, codec)
     if a.config == "c4":
         return run_c4(a, world, rank, local, dev, codec)
+    if a.config in ("scan", "scanmix"):
+        return run_scan(a, world, rank, local, dev, codec)
     import torch.distributed as dist
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import handles_tensor
@@ -370,6 +373,61 @@ def run_c4(a, world, rank, local, dev, codec):
                                "sample": "first %d pairs, restated BithashWriter.Add + golang/snappy Encode, 1 thread (%s)"
                                          % (m, cpu_info())}
         res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def run_scan(a, world, rank, local, dev, codec):
+    """Row A4: bhg_scan_tables (TableIterator.findEntry header chase, table.go:358-395)
+    over 1M records.  scan: uniform 32 B / 1 KiB records in 128 MiB tables (C2 data);
+    scanmix: values U[64, 4096] B (the C4 input, NoCompressor) -- every record a
+    different length, so the window chase does all the work."""
+    from bitalosdb_amd import synth
+    n = a.blocks
+    if a.config == "scan":
+        src, h, meta = synth.uniform_tables(n, device=dev, seed=synth_seed(rank))
+        tb = meta["table_bytes"]
+        toff = np.array([t * tb for t in range(meta["tables"])] + [meta["src_bytes"]], dtype=np.uint64)
+        what = "uniform 1076 B records, 128 MiB tables (C2 data)"
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(synth_seed(rank) + 7)
+        val_lens = torch.randint(64, 4097, (n,), generator=g, device=dev, dtype=torch.int64)
+        src, h, meta, bufs = _encode_tables(codec, n, val_lens, dev, synth_seed(rank), 0)
+        ts = bufs[-1].table_start.cpu().numpy().view(np.uint32)[:meta["ntables"]]
+        toff = np.array([int(h["offset"][i]) for i in ts] + [meta["src_bytes"]], dtype=np.uint64)
+        what = "values U[64, 4096] B, raw, 128 MiB tables (C4 input)"
+    ntab = len(toff) - 1
+    from bitalosdb_amd.codec import _u64_tensor
+    toff_t = _u64_tensor(toff, dev)
+    out_h, first, end = codec.scan_tables(src, toff_t, mode=0)
+    codec.sync()
+    got = out_h.cpu().numpy().view(np.uint8).reshape(-1).view(np.dtype([("offset", "<u8"), ("length", "<u4"), ("pad", "<u4")]))
+    par = len(got) == n and bool((got["offset"] == h["offset"]).all() and (got["length"] == h["length"]).all())
+    step = lambda: codec.scan_tables(src, toff_t, mode=0, max_out=n)
+    el, kms = _timed(a, dev, step)
+    scanned = float(toff[-1])
+    res = {"metric": "GiB/s table data regions scanned (TableIterator header chase), 1 GPU",
+           "value": round(scanned * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": "row A4 table scan: " + what, "records_per_gpu": n, "tables": ntab,
+                      "bytes": int(scanned), "Mrecords_per_s": round(n * a.steps / el / 1e6, 2)},
+           "parity_vs_generator_handles": "bit-exact" if par else "MISMATCH"}
+    if rank == 0 and world == 1 and not a.no_cpu:
+        from oracle import oracle as O
+        host = src.cpu().numpy()
+        t = time.perf_counter()
+        done = 0
+        for ti in range(ntab):
+            O.scan_region(host[int(toff[ti]):int(toff[ti + 1])], mode=0, max_records=n)
+            done += int(toff[ti + 1] - toff[ti])
+            if time.perf_counter() - t > a.cpu_seconds:
+                break
+        cs = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": round(done / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": "bho_scan_region over %d B of the same tables, 1 thread (%s)"
+                                         % (done, cpu_info())}
     if rank == 0:
         print(json.dumps(res), flush=True)
 

@@ -355,4 +355,22 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     return BHG_OK;
 }
 
+int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                    bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (mode != 0 && mode != 1) { set_err(c, "bad scan mode %d", mode); return BHG_EINVAL; }
+    if (!out_first) { set_err(c, "scan needs out_first[ntables+1]"); return BHG_EINVAL; }
+    if (ntables == 0) return bhg_memset_device(c, out_first, 0, 8, stream);
+    if (!src || !table_off || (!out_handles && max_out)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(ntables))) return r;
+    }
+    HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end,
+                                 c->scratch));
+    return BHG_OK;
+}
+
 }  // extern "C"

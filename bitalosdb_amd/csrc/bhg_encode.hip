@@ -259,8 +259,3 @@ hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t
 }
 
 }  // namespace bhg
-
-extern "C" int bhg_scan_tables(bhg_ctx *, const uint8_t *, const uint64_t *, uint32_t, int, bhg_handle *, uint64_t,
-                               uint64_t *, uint64_t *, void *) {
-    return BHG_EINVAL;  // implemented in a later milestone
-}

@@ -68,4 +68,9 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
 size_t scan_scratch_bytes(uint64_t n);
 hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch);
 
+// bhg_tscan.hip: table data-region scan (count -> scan -> write); first[ntables+1],
+// scan_scratch holds scan_scratch_bytes(ntables).
+hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch);
+
 }  // namespace bhg

@@ -1,0 +1,178 @@
+// bhg_tscan.hip -- the sequential data-region scan of a .bht table on gfx950:
+// TableIterator.findEntry (bithash/table.go:358-395, mode 0) and
+// Writer.rebuild (bithash/writer.go:539-583, mode 1).
+//
+// A record's start depends on the previous header, so each
+// table is one dependency chain; one 1024-thread workgroup walks it.
+// Two moves alternate:
+//  * speculation (uniform record lengths -- the common bulk-load case):
+//    from a known start `off` with the last record length G, thread i reads
+//    the header at off + i*G.  Threads up to the first one whose length is
+//    not G (or that hits a stop rule) are all true record starts, and that
+//    first different one is a true start too: up to 1025 records per
+//    global-memory round trip.
+//  * window chase (mixed lengths): the workgroup stages the next 64 KiB of
+//    the table in LDS with coalesced loads and thread 0 follows the headers
+//    at LDS latency.
+// The scan runs twice: count per table -> exclusive scan (out_first) ->
+// the same walk again writing the handles.
+#include "bhg_device.h"
+#include "bhg_internal.h"
+
+namespace bhg {
+
+namespace {
+
+constexpr int TS_THREADS = 1024;
+constexpr int TS_WAVES = TS_THREADS / 64;
+constexpr uint32_t TS_WIN = 64 * 1024;
+
+struct Hdr {
+    bool stop;
+    uint64_t adv;  // bytes to the next record; the handle length is (uint32)adv
+};
+
+// Stop rules of bho_scan_region / the reference loops, given the remaining
+// table bytes `rem` at the record start and its header words k, v.
+__device__ __forceinline__ Hdr hdr_rule(uint64_t rem, uint32_t k, uint32_t v, int mode) {
+    Hdr h = {true, 0};
+    if (mode == 0) {
+        if (k == 0 || v == 0) return h;                     // table.go:373-375: end of data
+        const uint32_t kv = k + v;                          // uint32 arithmetic, table.go:377
+        if (rem - 12 < kv) return h;                        // short ReadAt of key+value -> error
+        h.stop = false;
+        h.adv = 12 + (uint64_t)kv;
+    } else {
+        if (k == 0) return h;                               // writer.go:558
+        if (rem - 12 < k) return h;                         // short key read
+        h.stop = false;
+        h.adv = 12 + (uint64_t)(uint32_t)(k + v);           // value may run past the end (writer.go:566-572)
+    }
+    return h;
+}
+
+__device__ __forceinline__ Hdr read_hdr_global(uint64_t t0, uint64_t tlen, uint64_t off, int mode) {
+    const uint64_t rem = tlen > off ? tlen - off : 0;
+    if (rem < 12) return Hdr{true, 0};                      // short header read
+    const uint64_t p = t0 + off, end = t0 + tlen;
+    return hdr_rule(rem, ldu32(p, end), ldu32(p + 4, end), mode);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *s) {
+    return (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict__ src,
+                                                      const uint64_t *__restrict__ table_off, int mode,
+                                                      bhg_handle *__restrict__ out, uint64_t max_out,
+                                                      uint64_t *__restrict__ first, uint64_t *__restrict__ out_end) {
+    __shared__ alignas(16) uint8_t win[TS_WIN];
+    __shared__ uint32_t s_brk[2][TS_WAVES];
+    __shared__ uint64_t s_adv[2][TS_WAVES];
+    __shared__ uint64_t s_off, s_cnt, s_G;
+    __shared__ int s_done;
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t t = blockIdx.x;
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase;
+    const uint64_t w0 = WRITE ? first[t] : 0;
+
+    uint64_t off = 0, cnt = 0, G = 0;
+    int par = 0;
+    for (;;) {
+        // ---- speculation step ----
+        const uint64_t po = off + (uint64_t)tid * G;
+        Hdr h = {true, 0};
+        if (tid == 0 || G != 0) h = read_hdr_global(t0, tlen, po, mode);
+        const bool same = G != 0 && !h.stop && h.adv == G;
+        const uint64_t brk = __ballot(!same);
+        const uint32_t wb = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+        if (lane == 0) s_brk[par][wv] = wb;
+        if (wb < 64 && lane == wb) s_adv[par][wv] = h.stop ? ~0ull : h.adv;
+        __syncthreads();
+        uint32_t a = TS_THREADS;
+        uint64_t adv_a = ~0ull;
+        for (int q = 0; q < TS_WAVES; q++) {
+            const uint32_t b = s_brk[par][q];
+            if (b < 64) {
+                a = 64 * q + b;
+                adv_a = s_adv[par][q];
+                break;
+            }
+        }
+        par ^= 1;  // the next step writes the other slot: no second barrier needed
+        if (WRITE && tid < a && w0 + cnt + tid < max_out)
+            out[w0 + cnt + tid] = bhg_handle{tbase + po, (uint32_t)G, 0};
+        cnt += a;
+        off += (uint64_t)a * G;
+        if (a == TS_THREADS) continue;
+        if (adv_a == ~0ull) break;  // record a hits a stop rule: the scan ends at its start
+        if (WRITE && tid == 0 && w0 + cnt < max_out) out[w0 + cnt] = bhg_handle{tbase + off, (uint32_t)adv_a, 0};
+        cnt += 1;
+        const uint64_t G_prev = G;
+        off += adv_a;
+        G = adv_a;
+        if (a >= 32 || G_prev == 0) continue;  // speculation still pays (or had no guess yet)
+
+        // ---- window chase: stage [off, off + TS_WIN) in LDS, thread 0 follows headers ----
+        const uint64_t wbeg = off;
+        const uint64_t wend = tlen > off ? (tlen - off < TS_WIN ? tlen : off + TS_WIN) : off;
+        const uint32_t wlen = (uint32_t)(wend - wbeg);
+        for (uint32_t b = tid * 16; b < wlen; b += TS_THREADS * 16) {
+            if (b + 16 <= wlen) {
+                *reinterpret_cast<u32x4_a4 *>(win + b) = gld<u32x4_a4>(t0 + wbeg + b);
+            } else {
+                for (uint32_t j = b; j < wlen; j++) win[j] = gld<uint8_t>(t0 + wbeg + j);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int done = 0;
+            for (;;) {
+                const uint64_t rem = tlen > off ? tlen - off : 0;
+                if (rem < 12) { done = 1; break; }
+                if (off + 8 > wend) break;  // header not staged: next step
+                const uint8_t *s = win + (off - wbeg);
+                const Hdr hh = hdr_rule(rem, lds_u32(s), lds_u32(s + 4), mode);
+                if (hh.stop) { done = 1; break; }
+                if (WRITE && w0 + cnt < max_out) out[w0 + cnt] = bhg_handle{tbase + off, (uint32_t)hh.adv, 0};
+                cnt += 1;
+                off += hh.adv;
+                G = hh.adv;
+            }
+            s_off = off;
+            s_cnt = cnt;
+            s_G = G;
+            s_done = done;
+        }
+        __syncthreads();
+        off = s_off;
+        cnt = s_cnt;
+        G = s_G;
+        if (s_done) break;
+        // the next chase overwrites win / s_*: every reader passes the speculation barrier first
+    }
+    if (tid == 0) {
+        if (!WRITE) first[t] = cnt;
+        else if (out_end) out_end[t] = off;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch) {
+    hipLaunchKernelGGL((k_tscan<false>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
+                       max_out, first, out_end);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = launch_exclusive_scan_u64(L, first, first, ntables, scan_scratch);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_tscan<true>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
+                       max_out, first, out_end);
+    return hipGetLastError();
+}
+
+}  // namespace bhg

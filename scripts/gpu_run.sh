@@ -16,6 +16,15 @@ for s in $STEPS; do
       timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
       [ $rc -eq 0 ] || exit $rc ;;
+    testf)
+      timeout -k 10 600 python -m pytest ${TESTF:-tests} -m gpu -x -q > $OUT/pytest_f.log 2>&1; rc=$?
+      echo "pytest rc=$rc" >> $OUT/pytest_f.log; tail -15 $OUT/pytest_f.log
+      [ $rc -eq 0 ] || exit $rc ;;
+    scan)
+      timeout -k 10 300 python bench.py --config scan --steps 10 --warmup 2 > $OUT/bench_scan.log 2>&1 || exit $?
+      cat $OUT/bench_scan.log
+      timeout -k 10 300 python bench.py --config scanmix --steps 10 --warmup 2 > $OUT/bench_scanmix.log 2>&1 || exit $?
+      cat $OUT/bench_scanmix.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
       cat $OUT/smoke.log ;;
