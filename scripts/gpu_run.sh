@@ -13,7 +13,7 @@ STEPS=${@:-"test bench prof"}
 for s in $STEPS; do
   case $s in
     test)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
       [ $rc -eq 0 ] || exit $rc ;;
     testf)
