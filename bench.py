@@ -172,7 +172,7 @@ def run(a, world, rank, local, dev, codec):
                    "codec": "none", "parallelism": "table-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "k_decode_lane<MODE_NONE,4,16,512,8,2>", "kernel_avg_ms": round(avg_kern_ms, 4),
+                     "kernel": "k_decode_tile<8>", "kernel_avg_ms": round(avg_kern_ms, 4),
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK},
         "status_ok_blocks": int(ok_total),
         "digest_all_ranks": "%016x" % digest_all,

@@ -12,6 +12,9 @@
 
 #include <mutex>
 
+#include <vector>
+
+#include "bhg_crc_tables.h"
 #include "bhg_internal.h"
 
 struct bhg_ctx {
@@ -28,6 +31,7 @@ struct bhg_ctx {
     // host (end-to-end) path device buffers
     void *h_src = nullptr; size_t h_src_cap = 0;
     void *h_aux = nullptr; size_t h_aux_cap = 0;
+    uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
 };
 
 namespace {
@@ -58,6 +62,7 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     L.lane_wgs_per_cu = c->lane_wgs_per_cu;
     L.variant = c->variant;
     L.snappy_variant = c->snappy_variant;
+    L.ztab = c->ztab;
     return L;
 }
 
@@ -107,7 +112,7 @@ bhg_ctx *bhg_create(int device, int flags) {
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     c->lane_wgs_per_cu = 0;
-    c->variant = 28;  // k_decode_lane: slice-4 x16, 128 B line-aligned prefetched windows (bhg_decode.hip)
+    c->variant = bhg::kTileVariant;  // k_decode_tile (bhg_decode_tile.hip); snappy header pass: lane variant 28
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
     if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
     c->snappy_variant = 0;
@@ -119,6 +124,17 @@ bhg_ctx *bhg_create(int device, int flags) {
         delete c;
         return nullptr;
     }
+    {
+        std::vector<uint32_t> z(bhg::kZTabWords);
+        bhg::build_tile_ztab(z.data());
+        if (hipMalloc(reinterpret_cast<void **>(&c->ztab), z.size() * 4) != hipSuccess ||
+            hipMemcpy(c->ztab, z.data(), z.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            if (c->ztab) hipFree(c->ztab);
+            hipStreamDestroy(c->stream);
+            delete c;
+            return nullptr;
+        }
+    }
     return c;
 }
 
@@ -129,6 +145,7 @@ void bhg_destroy(bhg_ctx *c) {
     if (c->scratch) hipFree(c->scratch);
     if (c->h_src) hipFree(c->h_src);
     if (c->h_aux) hipFree(c->h_aux);
+    if (c->ztab) hipFree(c->ztab);
     hipStreamDestroy(c->stream);
     delete c;
 }

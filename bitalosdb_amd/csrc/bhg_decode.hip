@@ -1134,6 +1134,8 @@ static void launch_lane_mode(const Launch &L, int variant, const uint8_t *src, u
 hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes) {
     int variant = L.variant;
+    if (codec == BHG_CODEC_NONE && variant == kTileVariant)
+        return launch_decode_tile(L, src, src_len, h, n, expected_crc, out);
     if (variant < 0 || variant >= kNumLaneVariants) variant = 28;
     if (codec == BHG_CODEC_NONE)
         launch_lane_mode<MODE_NONE>(L, variant, src, src_len, h, n, expected_crc, out, sizes);

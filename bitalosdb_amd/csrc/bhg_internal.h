@@ -14,6 +14,7 @@ struct Launch {
     int lane_wgs_per_cu;  // override of resident workgroups per CU (0 = variant default)
     int variant;          // lane-kernel variant (bhg_decode.hip kLaneVariants)
     int snappy_variant;   // 0: lane-per-block snappy decode, 1: wave-per-block
+    const uint32_t *ztab; // device copy of build_tile_ztab() (owned by the context)
 };
 
 // persistent grid for lane-per-block kernels: enough workgroups to fill the
@@ -28,6 +29,10 @@ inline uint32_t lane_grid(const Launch &L, uint64_t n, uint32_t block) {
 // bhg_decode.hip
 hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+// bhg_decode_tile.hip: default NoCompressor decode (variant kTileVariant)
+constexpr int kTileVariant = 44;
+hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                              const uint32_t *expected_crc, bhg_desc *out);
 hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

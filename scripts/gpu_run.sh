@@ -60,7 +60,9 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/$OUT/pmc1 -o run --output-format csv \
         -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $OUT/pmc1.log 2>&1 || exit $?
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $GRAFT_REPO_ROOT/$OUT/pmc2 -o run --output-format csv \
-        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $OUT/pmc2.log 2>&1 || exit $? ;;
+        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $OUT/pmc2.log 2>&1 || exit $?
+      python scripts/pmc_summarize.py $OUT/pmc1/run_counter_collection.csv $OUT/pmc2/run_counter_collection.csv \
+        "${PMC_KERNEL:-k_decode_tile<8>}" $OUT/pmc_decode_c2.json "C2 1M x 1076 B blocks; run $TAG" ;;
   esac
 done
 echo done

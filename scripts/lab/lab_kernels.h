@@ -1259,6 +1259,1083 @@ __global__ __launch_bounds__(1024) void k_ccompute(const uint8_t *__restrict__ s
     if (x == 0x12345678u) reinterpret_cast<uint32_t *>(out)[threadIdx.x] = x;
 }
 
+
+
+// header / key / trailer / FNV-1 from a record staged in LDS at byte offset a
+// (key_len <= 36 from 13 LDS dwords; longer keys fall back to global reads)
+__device__ __forceinline__ uint32_t keep_from(int32_t x) {  // bytes b >= x of a dword (x clamped to [0, 4])
+    const int32_t c = x < 0 ? 0 : (x > 4 ? 4 : x);
+    return (uint32_t)(0xffffffffull << (8 * c));
+}
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *B, uint32_t a) {
+    const uint32_t *W = reinterpret_cast<const uint32_t *>(B + (a & ~3u));
+    const uint32_t sh = a & 3u;
+    return sh ? __builtin_amdgcn_alignbyte(W[1], W[0], sh) : W[0];
+}
+__device__ __forceinline__ void parse_lds(RecHead &H, const uint8_t *B, uint32_t a, uint64_t p, uint32_t L,
+                                          uint64_t end) {
+    H.k = lds_u32(B, a);
+    H.v = lds_u32(B, a + 4);
+    H.fn = lds_u32(B, a + 8);
+    H.valid = L >= 12 && H.k != 0 && H.v != 0 && (uint64_t)12 + H.k + H.v == (uint64_t)L;
+    H.key_len = 0;
+    H.fnv = BHG_FNV_OFFSET;
+    H.trailer = 255;
+    if (H.valid && H.k >= 8) {
+        H.key_len = H.k - 8;
+        if (H.key_len <= 36) {
+            uint32_t rw[11];
+#pragma unroll
+            for (uint32_t t = 0; t < 11; t++) rw[t] = lds_u32(B, a + 12 + 4 * t);
+            uint32_t h = BHG_FNV_OFFSET;
+#pragma unroll
+            for (uint32_t t = 0; t < 9; t++)
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    const uint32_t hn = (h * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                    h = 4 * t + b < H.key_len ? hn : h;
+                }
+            H.fnv = h;
+            H.trailer = (uint64_t)lds_u32(B, a + 12 + H.key_len) | ((uint64_t)lds_u32(B, a + 16 + H.key_len) << 32);
+        } else {
+            H.fnv = fnv1_range(p + 12, H.key_len, end);
+            H.trailer = ldu64(p + 12 + H.k - 8, end);
+        }
+    }
+}
+
+// ============================================================== E8: LDS-staged groups, striped chunk CRC
+// A workgroup of G*S threads takes groups of G consecutive handles.  The
+// group's byte span [lo16, hi) is loaded with coalesced dwordx4 loads (one
+// group ahead, register staged) into an LDS buffer; every record is cut into
+// CH-byte windows aligned to its END (window 0 holds the head, left-padded
+// with zeros, and absorbs the 0xFFFFFFFF init by xoring it into the record's
+// first 4 bytes).  Thread (r, j) = (t % G, t / G) takes windows q = m-1-j,
+// m-1-j-S, ... of record r: each window's CRC (from 0) runs as 4 interleaved
+// 32 B chains folded with Z_32; windows are Horner-folded with Z_{S*CH}, and
+// the stripe's sum is moved to the record end with Z_{CH*j}.  The S stripe
+// sums are xor-reduced through LDS; thread (r, 0) parses the header from LDS
+// and writes the descriptor.  Lanes 0..31 of a 32-lane ds_read_b32 group are
+// 32 different records: data reads are bank-conflict free at odd word strides.
+// Groups whose span exceeds SPAN (scattered handles) fall back to a per-record
+// global walk by thread (r, 0).
+template <int G, int S, int CH, int R, int SPAN, int MODE>
+__global__ __launch_bounds__(G * S) void k_stage(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                 const bhg_handle *__restrict__ handles, uint32_t n,
+                                                 bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    static_assert(G == 32 && CH == 128 && (S & (S - 1)) == 0, "layout");
+    constexpr uint32_t NT = G * S;
+    constexpr uint32_t PAD = CH;                       // window 0 may start up to CH-1 bytes before the record
+    constexpr uint32_t BUFB = PAD + SPAN + 16;
+    constexpr uint32_t NV = (SPAN + 16 * NT - 1) / (16 * NT);  // dwordx4 per thread per group
+    constexpr int SB = S == 8 ? 3 : S == 4 ? 2 : S == 2 ? 1 : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t ST[2][BUFB];
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<R>::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[(2 + SB) * 1024];  // Z32, Z_{S*CH}, Z_{CH<<b}
+    __shared__ uint32_t RED[S][G];
+    __shared__ uint32_t MREL[2][G], ML[2][G], MFL[2][G];
+    __shared__ uint64_t SPLO[2];
+    __shared__ uint32_t SPNV[2];
+    Crc4Lds<R>::fill(T);
+    for (uint32_t t = threadIdx.x; t < (2 + SB) * 1024; t += NT) Z[t] = gz[t];
+    const Crc4Lds<R> crc(T);
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t r = tid % G, j = tid / G;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ngroups = (n + G - 1) / G;
+    const bool w0 = tid < 64;
+    auto zapply = [&](const uint32_t *Zt, uint32_t c) {
+        return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+    };
+    // wave 0, lanes < G: handle of group g -> meta slot b (+ span)
+    auto load_h = [&](uint32_t g) {
+        bhg_handle h = {0, 0, 0};
+        const uint32_t i = g * G + lane;
+        if (w0 && lane < G && g < ngroups && i < n) h = handles[i];
+        return h;
+    };
+    auto set_meta = [&](uint32_t g, const bhg_handle &h, int b) {
+        if (!w0) return;
+        const uint32_t i = g * G + lane;
+        uint32_t fl = 0;  // bit0 valid index, bit1 inb, bit2 staged, bits 8.. status
+        uint64_t lo = ~0ull, hi = 0;
+        if (lane < G && g < ngroups && i < n) {
+            fl = 1;
+            if (h.length == 0) fl |= BHG_ST_ILLEGAL_LENGTH << 8;
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) fl |= BHG_ST_INCOMPLETE << 8;
+            else { fl |= 2; lo = h.offset; hi = h.offset + h.length; }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t lo2 = shfl64(lo, lane ^ o), hi2 = shfl64(hi, lane ^ o);
+            lo = lo2 < lo ? lo2 : lo;
+            hi = hi2 > hi ? hi2 : hi;
+        }
+        const uint64_t lo16 = lo & ~15ull;
+        const bool fits = hi > lo && hi - lo16 <= SPAN;
+        if (lane < G) {
+            MREL[b][lane] = (uint32_t)(h.offset - lo16);
+            ML[b][lane] = h.length;
+            MFL[b][lane] = fl | ((fits && (fl & 2) && h.length >= 4) ? 4u : 0u);
+        }
+        if (lane == 0) {
+            SPLO[b] = lo16;
+            SPNV[b] = fits ? (uint32_t)((hi - lo16 + 15) >> 4) : 0u;
+        }
+    };
+    u32x4 pre[NV];
+    auto issue = [&](int b) {
+        const uint64_t a0 = base + SPLO[b];
+        const uint32_t nv = SPNV[b];
+        if (a0 + 16ull * nv <= end) {
+#pragma unroll
+            for (uint32_t k = 0; k < NV; k++) {
+                const uint32_t v = tid + k * NT;
+                if (v < nv) pre[k] = gld<u32x4>(a0 + 16ull * v);
+            }
+        } else {
+            for (uint32_t k = 0; k < NV; k++) {
+                const uint32_t v = tid + k * NT;
+                const uint64_t a = a0 + 16ull * v;
+                if (v < nv)
+                    pre[k] = u32x4{ld32_safe(a, end), ld32_safe(a + 4, end), ld32_safe(a + 8, end), ld32_safe(a + 12, end)};
+            }
+        }
+    };
+    auto commit = [&](int b) {
+        const uint32_t nv = SPNV[b];
+#pragma unroll
+        for (uint32_t k = 0; k < NV; k++) {
+            const uint32_t v = tid + k * NT;
+            if (v < nv) *reinterpret_cast<u32x4 *>(&ST[b][PAD + 16 * v]) = pre[k];
+        }
+    };
+    uint32_t g = blockIdx.x;
+    const uint32_t gs = gridDim.x;
+    bhg_handle hn = load_h(g);
+    set_meta(g, hn, 0);
+    hn = load_h(g + gs);
+    __syncthreads();
+    issue(0);
+    commit(0);
+    set_meta(g + gs, hn, 1);
+    hn = load_h(g + 2 * gs);
+    __syncthreads();
+    for (int cur = 0; g < ngroups; g += gs, cur ^= 1) {
+        const int nxt = cur ^ 1;
+        if (g + gs < ngroups) issue(nxt);
+        // ---- striped window CRC over ST[cur]
+        const uint32_t fl = MFL[cur][r];
+        uint32_t acc = 0;
+        if (fl & 4) {
+            const uint32_t L = ML[cur][r], rel = MREL[cur][r];
+            const uint32_t m = (L + CH - 1) / CH;
+            if (j < m) {
+                const uint32_t qmax = m - 1 - j;
+                const uint32_t recend = PAD + rel + L;
+                const uint32_t zlead = CH * m - L;  // zero bytes before the record in window 0
+                for (int32_t q = (int32_t)(qmax % S); q <= (int32_t)qmax; q += S) {
+                    const uint32_t A = recend - CH * (m - (uint32_t)q);
+                    const uint32_t a0 = A & ~3u, sh = A & 3u;
+                    const uint32_t *W = reinterpret_cast<const uint32_t *>(&ST[cur][a0]);
+                    const int32_t zl = q == 0 ? (int32_t)zlead : -64;
+                    uint32_t Wd[CH / 4 + 1];
+#pragma unroll
+                    for (uint32_t t = 0; t <= CH / 4; t++) Wd[t] = W[t];
+                    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t t = 0; t < 8; t++) {
+#pragma unroll
+                        for (uint32_t k = 0; k < 4; k++) {
+                            const uint32_t wi = 8 * k + t;
+                            uint32_t w = __builtin_amdgcn_alignbyte(Wd[wi + 1], Wd[wi], sh);
+                            const int32_t zz = zl - 4 * (int32_t)wi;  // record start relative to this word
+                            const uint32_t k0 = keep_from(zz), k4 = keep_from(zz + 4);
+                            w = (w & k0) ^ (k0 & ~k4);
+                            c[k] = crc.word(c[k], w);
+                        }
+                    }
+                    uint32_t v = zapply(Z, c[0]) ^ c[1];
+                    v = zapply(Z, v) ^ c[2];
+                    v = zapply(Z, v) ^ c[3];
+                    acc = zapply(Z + 1024, acc) ^ v;
+                }
+#pragma unroll
+                for (int b = 0; b < SB; b++)
+                    if ((j >> b) & 1u) acc = zapply(Z + 2048 + 1024 * b, acc);
+            }
+        }
+        RED[j][r] = acc;
+        __syncthreads();
+        if (j == 0 && (fl & 1)) {
+            const uint32_t i = g * G + r;
+            DescOutL d = {0, 0, 0, 0, 0, 0, 0, 0, fl >> 8};
+            if (fl & 2) {
+                const uint32_t L = ML[cur][r];
+                const uint64_t p = base + SPLO[cur] + MREL[cur][r];
+                uint32_t state;
+                if (fl & 4) {
+                    state = 0;
+#pragma unroll
+                    for (int s2 = 0; s2 < S; s2++) state ^= RED[s2][r];
+                } else if (!(MODE & 1)) {
+                    state = crc_range_a<8, Crc4Lds<R>, true>(crc, 0xffffffffu, p, L, end);
+                } else {
+                    state = 0;
+                }
+                RecHead H;
+                if ((fl & 4) || (MODE & 1)) parse_lds(H, ST[cur], PAD + MREL[cur][r], p, L, end);
+                else H.parse(p, L, end);
+                d = H.desc(crc_mask(~state));
+            }
+            store_descL(out + i, d);
+        }
+        if (g + gs < ngroups) commit(nxt);
+        set_meta(g + 2 * gs, hn, cur);
+        hn = load_h(g + 3 * gs);
+        __syncthreads();
+    }
+}
+
+
+// ============================================================== E9: window-per-lane in registers, 8 lanes per record
+// A wave takes groups of 8 consecutive handles; lane (r, j) = (lane / 8,
+// lane % 8).  Record r is cut into its head [0, hl) (hl = L - 128 (m-1),
+// 1..128 B) and m-1 full 128-B windows aligned to its end.  Lane j owns the
+// windows q = m-1-j, m-1-j-8, ... (>= 1) and, when j == (m-1) % 8, the head.
+// Each lane loads its windows straight into registers (132 B from a
+// 4-aligned address: 64 lanes read one contiguous ~8.6 KB run per group),
+// CRCs them (the head from 0xFFFFFFFF, full windows from 0), Horner-folds
+// them with Z_1024, moves the sum to the record end with Z_{128 j} (three
+// conditional table steps) and the 8 lanes xor-reduce.  The head lane parses
+// the header / key / trailer / FNV-1 from its registers and writes the
+// descriptor.  The next group's handles are prefetched one group ahead.
+template <int WPB, int R, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_win(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                  const bhg_handle *__restrict__ handles, uint32_t n,
+                                                  bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<R>::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[5 * 1024];  // Z1024, Z128, Z256, Z512, Z32
+    Crc4Lds<R>::fill(T);
+    for (uint32_t t = threadIdx.x; t < 5 * 1024; t += 64 * WPB) Z[t] = gz[t];
+    const uint32_t *ZS32 = Z + 4096;
+    __syncthreads();
+    const Crc4Lds<R> crc(T);
+    auto zapply = [&](const uint32_t *Zt, uint32_t c) {
+        return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+    };
+    const uint32_t lane = threadIdx.x & 63, r = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ngroups = (n + 7) / 8;
+    const uint32_t gstride = gridDim.x * WPB;
+    uint32_t g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    bhg_handle hn = {0, 0, 0};
+    if (g < ngroups && g * 8 + r < n) hn = handles[g * 8 + r];
+    for (; g < ngroups; g += gstride) {
+        const bhg_handle h = hn;
+        const uint32_t i = g * 8 + r;
+        const uint32_t gn = g + gstride;
+        if (gn < ngroups && gn * 8 + r < n) hn = handles[gn * 8 + r];
+        const bool valid = i < n;
+        uint32_t st = BHG_ST_OK;
+        bool inb = false;
+        if (valid) {
+            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;
+            else inb = true;
+        }
+        const uint32_t L = inb ? h.length : 0u;
+        const uint64_t p = base + h.offset;
+        const uint32_t m = inb ? (L + 127) / 128 : 1u;
+        const uint32_t hl = L - 128 * (m - 1);
+        const uint32_t jh = (m - 1) & 7;  // head lane
+        const bool head = inb && j == jh;
+        const int32_t q0 = (int32_t)(m - 1) - (int32_t)j;  // my last window
+        // ---- loads: head (132 B from p & ~3) and first full window
+        uint32_t hw[33], fw[33];
+        const uint64_t ha = p & ~3ull;
+        const uint32_t hsh = (uint32_t)(p & 3);
+        if (head) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                hw[32] = gld<uint32_t>(ha + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        }
+        // full windows of this lane in ascending order: q = qf, qf + 8, ..., q0 (qf >= 1)
+        int32_t qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+        const uint64_t wsh_base = p + hl;  // start of window 1
+        const uint32_t wsh = (uint32_t)(wsh_base & 3);
+        auto load_win = [&](uint32_t *w, int32_t q) {
+            const uint64_t a = (wsh_base + 128ull * (uint32_t)(q - 1)) & ~3ull;
+            if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 v = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = v.x; w[4 * t + 1] = v.y; w[4 * t + 2] = v.z; w[4 * t + 3] = v.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+        const bool hasw = inb && q0 >= 1;
+        if (hasw) load_win(fw, qf);
+        // ---- head CRC (from init) + header parse
+        uint32_t acc = 0;
+        uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
+        uint64_t trailer = 255;
+        bool rvalid = false;
+        if (head) {
+            uint32_t c = 0xffffffffu;
+            const uint32_t nw = hl >> 2;
+            for (uint32_t t = 0; t < nw; t++) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) { wv = t == u ? hw[u] : wv; wn = t == u ? hw[u + 1] : wn; }
+                c = crc.word(c, __builtin_amdgcn_alignbyte(wn, wv, hsh));
+            }
+            if (hl & 3) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) { wv = nw == u ? hw[u] : wv; wn = nw == u ? hw[u + 1] : wn; }
+                c = crc.partial(c, __builtin_amdgcn_alignbyte(wn, wv, hsh), hl & 3);
+            }
+            acc = c;
+            // header from registers (record bytes [0, 128) are in hw when L allows)
+            uint32_t rw[14];
+#pragma unroll
+            for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
+            k = L >= 12 ? rw[0] : 0u;
+            v = L >= 12 ? rw[1] : 0u;
+            fn = L >= 12 ? rw[2] : 0u;
+            rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;
+            if (rvalid && k >= 8) {
+                key_len = k - 8;
+                if (key_len <= 36) {
+                    uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                    for (uint32_t t = 3; t < 12; t++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t hn2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                            hh = 4 * (t - 3) + b < key_len ? hn2 : hh;
+                        }
+                    fnv = hh;
+                    const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
+                    uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+                    for (uint32_t u = 3; u < 12; u++) {
+                        a0 = tw == u ? rw[u] : a0;
+                        a1 = tw == u ? rw[u + 1] : a1;
+                        a2 = tw == u ? rw[u + 2] : a2;
+                    }
+                    trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
+                              ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
+                } else {
+                    fnv = fnv1_range(p + 12, key_len, end);
+                    trailer = ldu64(p + 12 + k - 8, end);
+                }
+            }
+        }
+        // ---- full windows
+        if (hasw) {
+            for (int32_t q = qf;; q += 8) {
+                uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t t = 0; t < 8; t++)
+#pragma unroll
+                    for (uint32_t kk = 0; kk < 4; kk++) {
+                        const uint32_t wi = 8 * kk + t;
+                        c[kk] = crc.word(c[kk], __builtin_amdgcn_alignbyte(fw[wi + 1], fw[wi], wsh));
+                    }
+                // fold the 4 interleaved 32-B chains: V = Z96 c0 ^ Z64 c1 ^ Z32 c2 ^ c3, via Horner on Z32
+                uint32_t V = zapply(ZS32, c[0]) ^ c[1];
+                V = zapply(ZS32, V) ^ c[2];
+                V = zapply(ZS32, V) ^ c[3];
+                acc = zapply(Z, acc) ^ V;
+                if (q + 8 > q0) break;
+                load_win(fw, q + 8);
+            }
+        }
+        // ---- move to the record end (Z_{128 j}) and reduce over the 8 lanes
+        if (j & 1) acc = zapply(Z + 1024, acc);
+        if (j & 2) acc = zapply(Z + 2048, acc);
+        if (j & 4) acc = zapply(Z + 3072, acc);
+        acc ^= __shfl_xor(acc, 1, 64);
+        acc ^= __shfl_xor(acc, 2, 64);
+        acc ^= __shfl_xor(acc, 4, 64);
+        if (valid && j == jh) {
+            DescOutL d = {0, 0, 0, 0, 0, 0, 0, 0, st};
+            if (inb) {
+                const uint32_t crcv = crc_mask(~acc);
+                if (rvalid) d = DescOutL{12, key_len, 12 + k, v, trailer, fn, fnv, crcv, BHG_ST_OK};
+                else d = DescOutL{0, 0, 0, 0, 0, 0, 0, crcv, BHG_ST_RECORD_NIL};
+            }
+            store_descL(out + i, d);
+        }
+    }
+}
+
+
+// ============================================================== E10: two-phase tile (record lanes, then window lanes)
+// A wave takes tiles of 64 consecutive handles.
+// Phase 1, lane = record: handle, status, the record head [0, hl) (hl = L -
+// 128 (m-1), 1..128 B) and the header / key / trailer prefix are loaded into
+// registers; the head CRC (from 0xFFFFFFFF), the header checks, FNV-1 and the
+// trailer are computed by all 64 lanes at once.
+// Phase 2, 8 rounds of 8 records: lane (r, j) CRCs record 8s+r's full
+// 128-B windows q = m-1-j, m-1-j-8, ... (>= 1; 132 B loads, a contiguous
+// ~8.6 KB run per round), Horner-folds with Z_1024 starting from the head CRC
+// (fetched from phase 1) on lane j == (m-1) % 8, shifts by Z_{128 j}, and
+// the 8 lanes xor-reduce.  The next round's windows are loaded before the
+// current round is absorbed.
+template <int WPB, int R, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_tile(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                   const bhg_handle *__restrict__ handles, uint32_t n,
+                                                   bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<R>::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[5 * 1024];  // Z1024, Z128, Z256, Z512, Z32
+    Crc4Lds<R>::fill(T);
+    for (uint32_t t = threadIdx.x; t < 5 * 1024; t += 64 * WPB) Z[t] = gz[t];
+    __syncthreads();
+    const uint32_t *ZS32 = Z + 4096;
+    const Crc4Lds<R> crc(T);
+    auto zapply = [&](const uint32_t *Zt, uint32_t c) {
+        return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+    };
+    const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
+    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
+    bhg_handle hn = {0, 0, 0};
+    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    for (; tile < ntiles; tile += tstride) {
+        // ---------------- phase 1: lane = record
+        const bhg_handle h = hn;
+        const uint32_t i = tile * 64 + lane;
+        {
+            const uint32_t tn = tile + tstride;
+            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
+        }
+        const bool valid = i < n;
+        uint32_t st = BHG_ST_OK;
+        bool inb = false;
+        if (valid) {
+            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;
+            else inb = true;
+        }
+        const uint32_t L = inb ? h.length : 0u;
+        const uint64_t p = base + h.offset;
+        const uint32_t m = inb ? (L + 127) / 128 : 1u;
+        const uint32_t hl = L - 128 * (m - 1);
+        uint32_t hw[33];
+        const uint64_t ha = p & ~3ull;
+        const uint32_t hsh = (uint32_t)(p & 3);
+        if (inb) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                if (hl > 60) {
+#pragma unroll
+                    for (int t = 4; t < 8; t++) {
+                        const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                        hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                    }
+                    hw[32] = gld<uint32_t>(ha + 128);
+                } else {
+#pragma unroll
+                    for (int t = 16; t < 33; t++) hw[t] = 0;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        }
+        uint32_t hcrc = 0xffffffffu;
+        uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
+        uint64_t trailer = 255;
+        bool rvalid = false;
+        if (inb) {
+            const uint32_t nw = hl >> 2;
+#pragma unroll
+            for (uint32_t u = 0; u < 32; u++)
+                if (u < nw) hcrc = crc.word(hcrc, __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh));
+            if (hl & 3) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) { wv = nw == u ? hw[u] : wv; wn = nw == u ? hw[u + 1] : wn; }
+                hcrc = crc.partial(hcrc, __builtin_amdgcn_alignbyte(wn, wv, hsh), hl & 3);
+            }
+            uint32_t rw[14];
+#pragma unroll
+            for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
+            k = L >= 12 ? rw[0] : 0u;
+            v = L >= 12 ? rw[1] : 0u;
+            fn = L >= 12 ? rw[2] : 0u;
+            rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;
+            if (rvalid && k >= 8) {
+                key_len = k - 8;
+                if (key_len <= 36) {
+                    uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                    for (uint32_t t = 3; t < 12; t++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t hn2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                            hh = 4 * (t - 3) + b < key_len ? hn2 : hh;
+                        }
+                    fnv = hh;
+                    const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
+                    uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+                    for (uint32_t u = 3; u < 12; u++) {
+                        a0 = tw == u ? rw[u] : a0;
+                        a1 = tw == u ? rw[u + 1] : a1;
+                        a2 = tw == u ? rw[u + 2] : a2;
+                    }
+                    trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
+                              ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
+                } else {
+                    fnv = fnv1_range(p + 12, key_len, end);
+                    trailer = ldu64(p + 12 + k - 8, end);
+                }
+            }
+        }
+        // ---------------- phase 2: 8 rounds, lane (rr, j) on record 8s + rr
+        uint32_t mycrc = 0;
+        uint32_t fw[2][33];
+        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
+            const uint32_t src_l = 8 * s + rr;
+            const uint32_t Lr = __shfl(L, src_l, 64);
+            const uint64_t pr = shfl64(p, src_l);
+            mm = __shfl(m, src_l, 64);
+            const uint32_t hlr = Lr - 128 * (mm - 1);
+            wb = pr + hlr;
+            q0 = (int32_t)(mm - 1) - (int32_t)j;
+            hasw = Lr != 0 && q0 >= 1;
+            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+        };
+        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
+            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
+            if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+        uint64_t wb;
+        uint32_t mm;
+        int32_t qf, q0;
+        bool hasw;
+        rinfo(0, wb, mm, qf, q0, hasw);
+        if (hasw) load_win(fw[0], wb, qf);
+#pragma unroll
+        for (uint32_t s = 0; s < 8; s++) {
+            const uint32_t cb = s & 1;
+            const uint64_t wb_c = wb;
+            const uint32_t mm_c = mm;
+            const int32_t qf_c = qf, q0_c = q0;
+            const bool hasw_c = hasw;
+            if (s + 1 < 8) {
+                rinfo(s + 1, wb, mm, qf, q0, hasw);
+                if (hasw) load_win(fw[cb ^ 1], wb, qf);
+            }
+            const uint32_t hc = __shfl(hcrc, 8 * s + rr, 64);
+            uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
+            if (hasw_c) {
+                const uint32_t wsh = (uint32_t)(wb_c & 3);
+                for (int32_t q = qf_c;; q += 8) {
+                    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t t = 0; t < 8; t++)
+#pragma unroll
+                        for (uint32_t kk = 0; kk < 4; kk++) {
+                            const uint32_t wi = 8 * kk + t;
+                            c[kk] = crc.word(c[kk], __builtin_amdgcn_alignbyte(fw[cb][wi + 1], fw[cb][wi], wsh));
+                        }
+                    uint32_t V = zapply(ZS32, c[0]) ^ c[1];
+                    V = zapply(ZS32, V) ^ c[2];
+                    V = zapply(ZS32, V) ^ c[3];
+                    acc = zapply(Z, acc) ^ V;
+                    if (q + 8 > q0_c) break;
+                    load_win(fw[cb], wb_c, q + 8);
+                }
+            }
+            if (j & 1) acc = zapply(Z + 1024, acc);
+            if (j & 2) acc = zapply(Z + 2048, acc);
+            if (j & 4) acc = zapply(Z + 3072, acc);
+            acc ^= __shfl_xor(acc, 1, 64);
+            acc ^= __shfl_xor(acc, 2, 64);
+            acc ^= __shfl_xor(acc, 4, 64);
+            // record 8s + rr's total is on lanes 8 rr .. 8 rr + 7; lane l = 8 s + r takes lane 8 r
+            const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);
+            if ((lane >> 3) == s) mycrc = got;
+        }
+        if (valid) {
+            DescOutL d = {0, 0, 0, 0, 0, 0, 0, 0, st};
+            if (inb) {
+                const uint32_t crcv = crc_mask(~mycrc);
+                if (rvalid) d = DescOutL{12, key_len, 12 + k, v, trailer, fn, fnv, crcv, BHG_ST_OK};
+                else d = DescOutL{0, 0, 0, 0, 0, 0, 0, crcv, BHG_ST_RECORD_NIL};
+            }
+            store_descL(out + i, d);
+        }
+    }
+}
+
+template <int WPB, class Tab, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_tile2(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                   const bhg_handle *__restrict__ handles, uint32_t n,
+                                                   bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Tab::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[5 * 1024];  // Z1024, Z128, Z256, Z512, Z32
+    Tab::fill(T);
+    for (uint32_t t = threadIdx.x; t < 5 * 1024; t += 64 * WPB) Z[t] = gz[t];
+    __syncthreads();
+    const uint32_t *ZS32 = Z + 4096;
+    const Tab crc(T);
+    auto zapply = [&](const uint32_t *Zt, uint32_t c) {
+        return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+    };
+    const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
+    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
+    bhg_handle hn = {0, 0, 0};
+    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    for (; tile < ntiles; tile += tstride) {
+        // ---------------- phase 1: lane = record
+        const bhg_handle h = hn;
+        const uint32_t i = tile * 64 + lane;
+        {
+            const uint32_t tn = tile + tstride;
+            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
+        }
+        const bool valid = i < n;
+        uint32_t st = BHG_ST_OK;
+        bool inb = false;
+        if (valid) {
+            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;
+            else inb = true;
+        }
+        const uint32_t L = inb ? h.length : 0u;
+        const uint64_t p = base + h.offset;
+        const uint32_t m = inb ? (L + 127) / 128 : 1u;
+        const uint32_t hl = L - 128 * (m - 1);
+        uint32_t hw[33];
+        const uint64_t ha = p & ~3ull;
+        const uint32_t hsh = (uint32_t)(p & 3);
+        if (inb && (MODE & 8)) {  // diag: no phase-1 loads (synthetic header of a valid C2 record)
+#pragma unroll
+            for (int t = 0; t < 33; t++) hw[t] = t == 0 ? 40u : t == 1 ? 1024u : (uint32_t)p + t;
+        } else if (inb) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                if (hl > 60) {
+#pragma unroll
+                    for (int t = 4; t < 8; t++) {
+                        const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                        hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                    }
+                    hw[32] = gld<uint32_t>(ha + 128);
+                } else {
+#pragma unroll
+                    for (int t = 16; t < 33; t++) hw[t] = 0;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        }
+        uint32_t hcrc = 0xffffffffu;
+        uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
+        uint64_t trailer = 255;
+        bool rvalid = false;
+        if (inb) {
+            const uint32_t nw = hl >> 2;
+#pragma unroll
+            for (uint32_t u = 0; u < 32; u++)
+                if (u < nw) hcrc = crc.word(hcrc, __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh));
+            if (hl & 3) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) { wv = nw == u ? hw[u] : wv; wn = nw == u ? hw[u + 1] : wn; }
+                hcrc = crc.partial(hcrc, __builtin_amdgcn_alignbyte(wn, wv, hsh), hl & 3);
+            }
+            uint32_t rw[14];
+#pragma unroll
+            for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
+            k = L >= 12 ? rw[0] : 0u;
+            v = L >= 12 ? rw[1] : 0u;
+            fn = L >= 12 ? rw[2] : 0u;
+            rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;
+            if (rvalid && k >= 8) {
+                key_len = k - 8;
+                if (key_len <= 36) {
+                    uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                    for (uint32_t t = 3; t < 12; t++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t hn2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                            hh = 4 * (t - 3) + b < key_len ? hn2 : hh;
+                        }
+                    fnv = hh;
+                    const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
+                    uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+                    for (uint32_t u = 3; u < 12; u++) {
+                        a0 = tw == u ? rw[u] : a0;
+                        a1 = tw == u ? rw[u + 1] : a1;
+                        a2 = tw == u ? rw[u + 2] : a2;
+                    }
+                    trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
+                              ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
+                } else {
+                    fnv = fnv1_range(p + 12, key_len, end);
+                    trailer = ldu64(p + 12 + k - 8, end);
+                }
+            }
+        }
+        // ---------------- phase 2: 8 rounds, lane (rr, j) on record 8s + rr
+        uint32_t mycrc = 0;
+        uint32_t fw[2][33];  // MODE & 1: next round loaded after this round is absorbed
+        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
+            const uint32_t src_l = 8 * s + rr;
+            const uint32_t Lr = __shfl(L, src_l, 64);
+            const uint64_t pr = shfl64(p, src_l);
+            mm = __shfl(m, src_l, 64);
+            const uint32_t hlr = Lr - 128 * (mm - 1);
+            wb = pr + hlr;
+            q0 = (int32_t)(mm - 1) - (int32_t)j;
+            hasw = Lr != 0 && q0 >= 1;
+            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+        };
+        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
+            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
+            if (MODE & 2) {  // diag: compute only
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = (uint32_t)a * 0x9e3779b9u + t;
+            } else if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+        uint64_t wb;
+        uint32_t mm;
+        int32_t qf, q0;
+        bool hasw;
+        rinfo(0, wb, mm, qf, q0, hasw);
+        if (hasw) load_win(fw[0], wb, qf);
+#pragma unroll
+        for (uint32_t s = 0; s < 8; s++) {
+            const uint32_t cb = (MODE & 1) ? 0u : (s & 1);
+            const uint64_t wb_c = wb;
+            const uint32_t mm_c = mm;
+            const int32_t qf_c = qf, q0_c = q0;
+            const bool hasw_c = hasw;
+            if (!(MODE & 1) && s + 1 < 8) {
+                rinfo(s + 1, wb, mm, qf, q0, hasw);
+                if (hasw) load_win(fw[cb ^ 1], wb, qf);
+            }
+            const uint32_t hc = __shfl(hcrc, 8 * s + rr, 64);
+            uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
+            if (hasw_c) {
+                const uint32_t wsh = (uint32_t)(wb_c & 3);
+                for (int32_t q = qf_c;; q += 8) {
+                    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t t = 0; t < 8; t++)
+#pragma unroll
+                        for (uint32_t kk = 0; kk < 4; kk++) {
+                            const uint32_t wi = 8 * kk + t;
+                            const uint32_t wv = __builtin_amdgcn_alignbyte(fw[cb][wi + 1], fw[cb][wi], wsh);
+                            c[kk] = (MODE & 4) ? (((c[kk] << 1) | (c[kk] >> 31)) ^ wv) : crc.word(c[kk], wv);
+                        }
+                    uint32_t V = zapply(ZS32, c[0]) ^ c[1];
+                    V = zapply(ZS32, V) ^ c[2];
+                    V = zapply(ZS32, V) ^ c[3];
+                    acc = zapply(Z, acc) ^ V;
+                    if (q + 8 > q0_c) break;
+                    load_win(fw[cb], wb_c, q + 8);
+                }
+            }
+            if ((MODE & 1) && s + 1 < 8) {
+                rinfo(s + 1, wb, mm, qf, q0, hasw);
+                if (hasw) load_win(fw[0], wb, qf);
+            }
+            if (j & 1) acc = zapply(Z + 1024, acc);
+            if (j & 2) acc = zapply(Z + 2048, acc);
+            if (j & 4) acc = zapply(Z + 3072, acc);
+            acc ^= __shfl_xor(acc, 1, 64);
+            acc ^= __shfl_xor(acc, 2, 64);
+            acc ^= __shfl_xor(acc, 4, 64);
+            // record 8s + rr's total is on lanes 8 rr .. 8 rr + 7; lane l = 8 s + r takes lane 8 r
+            const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);
+            if ((lane >> 3) == s) mycrc = got;
+        }
+        if (valid) {
+            DescOutL d = {0, 0, 0, 0, 0, 0, 0, 0, st};
+            if (inb) {
+                const uint32_t crcv = crc_mask(~mycrc);
+                if (rvalid) d = DescOutL{12, key_len, 12 + k, v, trailer, fn, fnv, crcv, BHG_ST_OK};
+                else d = DescOutL{0, 0, 0, 0, 0, 0, 0, crcv, BHG_ST_RECORD_NIL};
+            }
+            store_descL(out + i, d);
+        }
+    }
+}
+
+template <int WPB, class Tab, int MODE, int PD>
+__global__ __launch_bounds__(64 * WPB) void k_tile3(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                   const bhg_handle *__restrict__ handles, uint32_t n,
+                                                   bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Tab::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[5 * 1024];  // Z1024, Z128, Z256, Z512, Z32
+    Tab::fill(T);
+    for (uint32_t t = threadIdx.x; t < 5 * 1024; t += 64 * WPB) Z[t] = gz[t];
+    __syncthreads();
+    const uint32_t *ZS32 = Z + 4096;
+    const Tab crc(T);
+    auto zapply = [&](const uint32_t *Zt, uint32_t c) {
+        return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+    };
+    const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
+    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
+    bhg_handle hn = {0, 0, 0};
+    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    for (; tile < ntiles; tile += tstride) {
+        // ---------------- phase 1: lane = record
+        const bhg_handle h = hn;
+        const uint32_t i = tile * 64 + lane;
+        {
+            const uint32_t tn = tile + tstride;
+            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
+        }
+        const bool valid = i < n;
+        uint32_t st = BHG_ST_OK;
+        bool inb = false;
+        if (valid) {
+            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;
+            else inb = true;
+        }
+        const uint32_t L = inb ? h.length : 0u;
+        const uint64_t p = base + h.offset;
+        const uint32_t m = inb ? (L + 127) / 128 : 1u;
+        const uint32_t hl = L - 128 * (m - 1);
+        uint32_t hw[33];
+        const uint64_t ha = p & ~3ull;
+        const uint32_t hsh = (uint32_t)(p & 3);
+        if (inb && (MODE & 8)) {  // diag: no phase-1 loads (synthetic header of a valid C2 record)
+#pragma unroll
+            for (int t = 0; t < 33; t++) hw[t] = t == 0 ? 40u : t == 1 ? 1024u : (uint32_t)p + t;
+        } else if (inb) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                if (hl > 60) {
+#pragma unroll
+                    for (int t = 4; t < 8; t++) {
+                        const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                        hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                    }
+                    hw[32] = gld<uint32_t>(ha + 128);
+                } else {
+#pragma unroll
+                    for (int t = 16; t < 33; t++) hw[t] = 0;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        }
+        uint32_t hcrc = 0xffffffffu;
+        uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
+        uint64_t trailer = 255;
+        bool rvalid = false;
+        if (inb) {
+            const uint32_t nw = hl >> 2;
+#pragma unroll
+            for (uint32_t u = 0; u < 32; u++)
+                if (u < nw) hcrc = crc.word(hcrc, __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh));
+            if (hl & 3) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) { wv = nw == u ? hw[u] : wv; wn = nw == u ? hw[u + 1] : wn; }
+                hcrc = crc.partial(hcrc, __builtin_amdgcn_alignbyte(wn, wv, hsh), hl & 3);
+            }
+            uint32_t rw[14];
+#pragma unroll
+            for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
+            k = L >= 12 ? rw[0] : 0u;
+            v = L >= 12 ? rw[1] : 0u;
+            fn = L >= 12 ? rw[2] : 0u;
+            rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;
+            if (rvalid && k >= 8) {
+                key_len = k - 8;
+                if (key_len <= 36) {
+                    uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                    for (uint32_t t = 3; t < 12; t++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t hn2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                            hh = 4 * (t - 3) + b < key_len ? hn2 : hh;
+                        }
+                    fnv = hh;
+                    const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
+                    uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+                    for (uint32_t u = 3; u < 12; u++) {
+                        a0 = tw == u ? rw[u] : a0;
+                        a1 = tw == u ? rw[u + 1] : a1;
+                        a2 = tw == u ? rw[u + 2] : a2;
+                    }
+                    trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
+                              ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
+                } else {
+                    fnv = fnv1_range(p + 12, key_len, end);
+                    trailer = ldu64(p + 12 + k - 8, end);
+                }
+            }
+        }
+        // ---------------- phase 2: 8 rounds, lane (rr, j) on record 8s + rr
+        uint32_t mycrc = 0;
+        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
+            const uint32_t src_l = 8 * s + rr;
+            const uint32_t Lr = __shfl(L, src_l, 64);
+            const uint64_t pr = shfl64(p, src_l);
+            mm = __shfl(m, src_l, 64);
+            const uint32_t hlr = Lr - 128 * (mm - 1);
+            wb = pr + hlr;
+            q0 = (int32_t)(mm - 1) - (int32_t)j;
+            hasw = Lr != 0 && q0 >= 1;
+            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+        };
+        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
+            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
+            if (MODE & 2) {  // diag: compute only
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = (uint32_t)a * 0x9e3779b9u + t;
+            } else if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+        constexpr int NB = PD + 1;
+        uint32_t fwb[NB][33];
+        uint64_t wbA[NB];
+        uint32_t mmA[NB];
+        int32_t qfA[NB], q0A[NB];
+        bool hasA[NB];
+#pragma unroll
+        for (int s0 = 0; s0 < PD; s0++) {
+            rinfo(s0, wbA[s0], mmA[s0], qfA[s0], q0A[s0], hasA[s0]);
+            if (hasA[s0]) load_win(fwb[s0], wbA[s0], qfA[s0]);
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < 8; s++) {
+            const int cb = s % NB;
+            if (s + PD < 8) {
+                const int nb = (s + PD) % NB;
+                rinfo(s + PD, wbA[nb], mmA[nb], qfA[nb], q0A[nb], hasA[nb]);
+                if (hasA[nb]) load_win(fwb[nb], wbA[nb], qfA[nb]);
+            }
+            const uint64_t wb_c = wbA[cb];
+            const uint32_t mm_c = mmA[cb];
+            const int32_t qf_c = qfA[cb], q0_c = q0A[cb];
+            const bool hasw_c = hasA[cb];
+            const uint32_t hc = __shfl(hcrc, 8 * s + rr, 64);
+            uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
+            if (hasw_c) {
+                const uint32_t wsh = (uint32_t)(wb_c & 3);
+                for (int32_t q = qf_c;; q += 8) {
+                    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t t = 0; t < 8; t++)
+#pragma unroll
+                        for (uint32_t kk = 0; kk < 4; kk++) {
+                            const uint32_t wi = 8 * kk + t;
+                            const uint32_t wv = __builtin_amdgcn_alignbyte(fwb[cb][wi + 1], fwb[cb][wi], wsh);
+                            c[kk] = (MODE & 4) ? (((c[kk] << 1) | (c[kk] >> 31)) ^ wv) : crc.word(c[kk], wv);
+                        }
+                    uint32_t V = zapply(ZS32, c[0]) ^ c[1];
+                    V = zapply(ZS32, V) ^ c[2];
+                    V = zapply(ZS32, V) ^ c[3];
+                    acc = zapply(Z, acc) ^ V;
+                    if (q + 8 > q0_c) break;
+                    load_win(fwb[cb], wb_c, q + 8);
+                }
+            }
+            if (j & 1) acc = zapply(Z + 1024, acc);
+            if (j & 2) acc = zapply(Z + 2048, acc);
+            if (j & 4) acc = zapply(Z + 3072, acc);
+            acc ^= __shfl_xor(acc, 1, 64);
+            acc ^= __shfl_xor(acc, 2, 64);
+            acc ^= __shfl_xor(acc, 4, 64);
+            // record 8s + rr's total is on lanes 8 rr .. 8 rr + 7; lane l = 8 s + r takes lane 8 r
+            const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);
+            if ((lane >> 3) == s) mycrc = got;
+        }
+        if (valid) {
+            DescOutL d = {0, 0, 0, 0, 0, 0, 0, 0, st};
+            if (inb) {
+                const uint32_t crcv = crc_mask(~mycrc);
+                if (rvalid) d = DescOutL{12, key_len, 12 + k, v, trailer, fn, fnv, crcv, BHG_ST_OK};
+                else d = DescOutL{0, 0, 0, 0, 0, 0, 0, crcv, BHG_ST_RECORD_NIL};
+            }
+            if (!(MODE & 16)) store_descL(out + i, d);
+            else if (d.crc == 0x12345678u) reinterpret_cast<uint32_t *>(out)[lane] = d.fnv1;
+        }
+    }
+}
+
 // ============================================================== launchers
 static int g_cus = 256;
 constexpr uint32_t kLabShiftSets = 3;  // CH = 64, 128, 256
@@ -1268,7 +2345,9 @@ constexpr size_t kLabBraidSet = 6 * 1024;                                // brai
 constexpr size_t kLabZ128Off = kLabBraidOff + 5 * kLabBraidSet;
 constexpr size_t kLabPlainOff = kLabZ128Off + 1024;   // plain slice-by-4 then Z128 (sweep2 layout)
 constexpr size_t kLabL5Off = kLabPlainOff + 2048;     // plain slice-by-4, Z4..Z128
-constexpr size_t kLabTabBytes = (kLabL5Off + 7 * 1024) * 4;
+constexpr size_t kLabStageOff = kLabL5Off + 7 * 1024;  // Z32, Z1024, Z128, Z256, Z512 (k_stage, S = 8)
+constexpr size_t kLabWinOff = kLabStageOff + 5 * 1024;  // Z1024, Z128, Z256, Z512, Z32 (k_win)
+constexpr size_t kLabTabBytes = (kLabWinOff + 5 * 1024) * 4;
 static void lab_init_tables(uint32_t *d) {
     std::vector<uint32_t> h(kLabTabBytes / 4);
     const uint32_t chs[3] = {64, 128, 256};
@@ -1287,6 +2366,12 @@ static void lab_init_tables(uint32_t *d) {
     for (uint32_t k = 0; k < 4; k++)
         for (uint32_t b = 0; b < 256; b++) h[kLabL5Off + k * 256 + b] = crc32c_tk(k, b);
     for (uint32_t j = 0; j < 6; j++) crc32c_shift_table(4ull << j, &h[kLabL5Off + 1024 * (1 + j)]);
+    {
+        const uint64_t zs[5] = {32, 1024, 128, 256, 512};
+        for (uint32_t k = 0; k < 5; k++) crc32c_shift_table(zs[k], &h[kLabStageOff + 1024 * k]);
+        const uint64_t zw[5] = {1024, 128, 256, 512, 32};
+        for (uint32_t k = 0; k < 5; k++) crc32c_shift_table(zw[k], &h[kLabWinOff + 1024 * k]);
+    }
     CK(hipMemcpy(d, h.data(), kLabTabBytes, hipMemcpyHostToDevice));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
@@ -1403,12 +2488,88 @@ static void L_lane5(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_
     hipLaunchKernelGGL((k_lane5<WG, MODE>), dim3(grid), dim3(WG), 0, st, s, len, h, n, o, tabs + kLabL5Off);
 }
 
+template <int R, int MODE, int WPC = 1>
+static void L_stage(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                    hipStream_t st) {
+    const uint32_t ng = (n + 31) / 32;
+    uint32_t grid = std::min<uint32_t>(ng, g_cus * WPC);
+    hipLaunchKernelGGL((k_stage<32, 8, 128, R, 34816, MODE>), dim3(grid), dim3(256), 0, st, s, len, h, n, o,
+                       tabs + kLabStageOff);
+}
+
+template <int WPB, int R, int MODE, int WPC = 1>
+static void L_win(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                  hipStream_t st) {
+    const uint32_t ng = (n + 7) / 8;
+    uint32_t grid = std::min<uint32_t>((ng + WPB - 1) / WPB, g_cus * WPC);
+    hipLaunchKernelGGL((k_win<WPB, R, MODE>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
+}
+
+template <int WPB, int R, int MODE, int WPC = 1>
+static void L_tile(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                   hipStream_t st) {
+    const uint32_t nt = (n + 63) / 64;
+    uint32_t grid = std::min<uint32_t>((nt + WPB - 1) / WPB, g_cus * WPC);
+    hipLaunchKernelGGL((k_tile<WPB, R, MODE>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
+}
+
+template <int WPB, class Tab, int MODE, int WPC = 1>
+static void L_tile2(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                    hipStream_t st) {
+    const uint32_t nt = (n + 63) / 64;
+    uint32_t grid = std::min<uint32_t>((nt + WPB - 1) / WPB, g_cus * WPC);
+    hipLaunchKernelGGL((k_tile2<WPB, Tab, MODE>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
+}
+
+template <int WPB, class Tab, int MODE, int PD, int WPC = 1>
+static void L_tile3(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                    hipStream_t st) {
+    const uint32_t nt = (n + 63) / 64;
+    uint32_t grid = std::min<uint32_t>((nt + WPB - 1) / WPB, g_cus * WPC);
+    hipLaunchKernelGGL((k_tile3<WPB, Tab, MODE, PD>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
+}
+
 struct LabEntry {
     const char *name;
     launch_fn fn;
     bool diag;
 };
 static const LabEntry kLab[] = {
+    {"tile3_w8_pd2", L_tile3<8, Crc4Perm, 0, 2>, false},
+    {"tile3_w8_pd3", L_tile3<8, Crc4Perm, 0, 3>, false},
+    {"tile3_w8_pd1", L_tile3<8, Crc4Perm, 0, 1>, false},
+    {"tile3_w8_pd2_loads_nop1", L_tile3<8, Crc4Perm, 4 | 8, 2>, true},
+    {"tile3_w8_pd3_loads_nop1", L_tile3<8, Crc4Perm, 4 | 8, 3>, true},
+    {"tile3_w8_pd2_loads_nop1_nod", L_tile3<8, Crc4Perm, 4 | 8 | 16, 2>, true},
+    {"tile3_w8_pd1_loads_nop1_nod", L_tile3<8, Crc4Perm, 4 | 8 | 16, 1>, true},
+    {"tile3_w8_pd2_nod", L_tile3<8, Crc4Perm, 16, 2>, true},
+    {"tile2_perm_w8_compute", L_tile2<8, Crc4Perm, 2, 1>, true},
+    {"tile2_perm_w8_loads", L_tile2<8, Crc4Perm, 4, 1>, true},
+    {"tile2_perm_w16_sb_compute", L_tile2<16, Crc4Perm, 3, 1>, true},
+    {"tile2_perm_w16_sb_loads", L_tile2<16, Crc4Perm, 5, 1>, true},
+    {"tile2_perm_w8_loads_nop1", L_tile2<8, Crc4Perm, 4 | 8, 1>, true},
+    {"tile2_perm_w8_nop1", L_tile2<8, Crc4Perm, 8, 1>, true},
+    {"tile2_perm_w16_sb_loads_nop1", L_tile2<16, Crc4Perm, 5 | 8, 1>, true},
+    {"tile2_perm_w16", L_tile2<16, Crc4Perm, 0, 1>, false},
+    {"tile2_perm_w16_sb", L_tile2<16, Crc4Perm, 1, 1>, false},
+    {"tile2_perm_w8", L_tile2<8, Crc4Perm, 0, 1>, false},
+    {"tile2_perm_w12_sb", L_tile2<12, Crc4Perm, 1, 1>, false},
+    {"tile2_r16_w8_sb", L_tile2<8, Crc4Lds<16>, 1, 2>, false},
+    {"tile_w4_r4_x4", L_tile<4, 4, 0, 4>, false},
+    {"tile_w4_r8_x3", L_tile<4, 8, 0, 3>, false},
+    {"tile_w8_r8_x2", L_tile<8, 8, 0, 2>, false},
+    {"tile_w8_r16_x2", L_tile<8, 16, 0, 2>, false},
+    {"tile_w16_r16_x1", L_tile<16, 16, 0, 1>, false},
+    {"tile_w4_r4_x8", L_tile<4, 4, 0, 8>, false},
+    {"win_w4_r4_x4", L_win<4, 4, 0, 4>, false},
+    {"win_w4_r8_x3", L_win<4, 8, 0, 3>, false},
+    {"win_w8_r16_x2", L_win<8, 16, 0, 2>, false},
+    {"win_w8_r8_x2", L_win<8, 8, 0, 2>, false},
+    {"win_w4_r4_x8", L_win<4, 4, 0, 8>, false},
+    {"win_w16_r16_x1", L_win<16, 16, 0, 1>, false},
+    {"stage_r8", L_stage<8, 0>, false},
+    {"stage_r16", L_stage<16, 0>, false},
+    {"stage_r8_nofb", L_stage<8, 1>, false},
     {"stream_u4_w8", L_stream<4, 8>, true},
     {"stream_u8_w8", L_stream<8, 8>, true},
     {"stream_u4_w16", L_stream<4, 16>, true},

@@ -274,7 +274,7 @@ def _full_size(codec, synth, handles_tensor, n):
     assert (got["trailer"] >> 8 == np.arange(1, n + 1)).all()
 
 
-@pytest.mark.parametrize("variant", [v for v in range(44) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
+@pytest.mark.parametrize("variant", [v for v in range(45) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
 def test_lane_kernel_variants(variant, monkeypatch):
     """Every CRC-table flavour of k_decode_lane is bit-exact (slice-by-1/4, R=4..32)."""
     from bitalosdb_amd.codec import BithashCodec
