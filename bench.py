@@ -179,15 +179,27 @@ def run(a, world, rank, local, dev, codec):
     }
 
     if rank == 0 and world == 1 and not a.no_e2e:
-        # end-to-end: host buffers (pageable) -> H2D -> kernel -> D2H descriptors
+        # end-to-end: host src -> H2D -> kernel -> D2H descriptors (bhg_decode_batch_host; handles are
+        # sorted, so the 64 MiB-chunk 3-stream pipeline runs).  Pageable first, then the same buffer
+        # page-locked with bhg_host_register (an mmap'd table file pinned once per mapping).
         host_src = src_t.cpu().numpy()
-        t = time.perf_counter()
-        reps = 2
-        for _ in range(reps):
-            codec.decode_host(host_src, h)
-        e2e_s = (time.perf_counter() - t) / reps
-        out["e2e_host"] = {"value": round(n * L / e2e_s / 2 ** 30, 3), "unit": "GiB/s",
-                           "note": "pageable host src (%.2f GB) + handles H2D, decode, 40 B/block D2H, synchronous"
+        e2e = {}
+        for mode in ("pageable", "pinned"):
+            if mode == "pinned":
+                codec.host_register(host_src)
+            codec.decode_host(host_src, h)      # warm the ring buffers
+            reps, t = 3, time.perf_counter()
+            for _ in range(reps):
+                got_host, _, _ = codec.decode_host(host_src, h)
+            e2e_s = (time.perf_counter() - t) / reps
+            e2e[mode] = round(n * L / e2e_s / 2 ** 30, 3)
+            if mode == "pinned":
+                codec.host_unregister(host_src)
+        host_ok = bool(np.array_equal(got_host["crc"], d["crc"]) and np.array_equal(got_host["status"], d["status"]))
+        out["e2e_host"] = {"value": e2e["pinned"], "unit": "GiB/s", "pageable": e2e["pageable"],
+                           "matches_device_path": host_ok,
+                           "note": "host src (%.2f GB) + handles H2D, decode, 40 B/block D2H; 64 MiB chunks over "
+                                   "3 streams; value = page-locked src (bhg_host_register), pageable also given"
                                    % (host_src.size / 1e9)}
     else:
         host_src = None

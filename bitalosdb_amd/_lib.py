@@ -30,6 +30,7 @@ EXPORTS = [
     "bhg_stream_sync", "bhg_malloc_device", "bhg_free_device", "bhg_malloc_host", "bhg_free_host",
     "bhg_memcpy_h2d", "bhg_memcpy_d2h", "bhg_memset_device", "bhg_decode_batch", "bhg_decode_batch_host",
     "bhg_crc32c_masked_batch", "bhg_fnv32_batch", "bhg_encode_batch", "bhg_scan_tables",
+    "bhg_host_register", "bhg_host_unregister",
 ]
 
 
@@ -82,6 +83,8 @@ def lib():
             "bhg_encode_batch": (I, [P, P, P, P, P, P, U32, I, P, U32, U32, U64, P, U64,
                                      ctypes.POINTER(EncodeOut), P]),
             "bhg_scan_tables": (I, [P, P, P, U32, I, P, U64, P, P, P]),
+            "bhg_host_register": (I, [P, P, U64]),
+            "bhg_host_unregister": (I, [P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -183,6 +183,13 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_decode_batch_host")
         return desc, (None if vals is None else vals[:int(off[-1])]), off
 
+    def host_register(self, arr):
+        """Pin a host numpy buffer (bhg_host_register) for DMA-rate *_host copies."""
+        B.check(self.ctx, self.L.bhg_host_register(self.ctx, _ptr(arr), arr.nbytes), "bhg_host_register")
+
+    def host_unregister(self, arr):
+        B.check(self.ctx, self.L.bhg_host_unregister(self.ctx, _ptr(arr)), "bhg_host_unregister")
+
     # ---- primitives ----
     def crc_batch(self, src_t, handles_t, n):
         with torch.cuda.stream(self.stream):

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -32,6 +33,11 @@ struct bhg_ctx {
     void *h_src = nullptr; size_t h_src_cap = 0;
     void *h_aux = nullptr; size_t h_aux_cap = 0;
     uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
+    // pipelined host path: kPipe slots, each with its own stream and device ring buffers
+    static constexpr int kPipe = 3;
+    hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
+    void *pbuf[kPipe] = {nullptr, nullptr, nullptr};
+    size_t pbuf_cap[kPipe] = {0, 0, 0};
 };
 
 namespace {
@@ -146,6 +152,10 @@ void bhg_destroy(bhg_ctx *c) {
     if (c->h_src) hipFree(c->h_src);
     if (c->h_aux) hipFree(c->h_aux);
     if (c->ztab) hipFree(c->ztab);
+    for (int k = 0; k < bhg_ctx::kPipe; k++) {
+        if (c->pstream[k]) { hipStreamSynchronize(c->pstream[k]); hipStreamDestroy(c->pstream[k]); }
+        if (c->pbuf[k]) hipFree(c->pbuf[k]);
+    }
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -240,6 +250,81 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     return BHG_OK;
 }
 
+namespace {
+
+// Pipelined end-to-end NoCompressor decode for handles sorted by offset (a
+// table scan, a compaction pass): the batch is cut into chunks of at most
+// kChunkBytes of src; chunk k goes to slot k % kPipe (own stream + device
+// buffer): H2D of its src byte range and handles, the decode kernel on the
+// rebased range, D2H of its descriptors.  Copies of one slot overlap the
+// kernels and copies of the others; slot reuse is ordered by its stream.
+constexpr uint64_t kChunkBytesDefault = 64ull << 20;
+
+int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                          const uint32_t *expected_crc, bhg_desc *out_desc) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    uint64_t kChunkBytes = kChunkBytesDefault;
+    if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) kChunkBytes = strtoull(e, nullptr, 10);  // tests
+    if (kChunkBytes < 4096) kChunkBytes = 4096;
+    const uint32_t max_chunk_n = 1u << 17;
+    const size_t need = al(kChunkBytes + 64) + al((size_t)max_chunk_n * sizeof(bhg_handle)) +
+                        al((size_t)max_chunk_n * sizeof(bhg_desc)) + al((size_t)max_chunk_n * 4);
+    for (int k = 0; k < bhg_ctx::kPipe; k++) {
+        if (!c->pstream[k]) HIP_TRY(c, hipStreamCreateWithFlags(&c->pstream[k], hipStreamNonBlocking));
+        if (int r = ensure_buf(c, &c->pbuf[k], &c->pbuf_cap[k], need)) return r;
+    }
+    bhg::Launch L = launch_of(c, nullptr);
+    uint32_t a = 0;
+    int slot = 0;
+    while (a < n) {
+        // grow the chunk while its byte span stays within kChunkBytes
+        uint64_t lo = UINT64_MAX, hi = 0;
+        uint32_t b = a;
+        while (b < n && b - a < max_chunk_n) {
+            const bhg_handle &h = handles[b];
+            const bool inb = h.length != 0 && h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
+            if (inb) {
+                const uint64_t nlo = h.offset < lo ? h.offset : lo;
+                const uint64_t nhi = h.offset + h.length > hi ? h.offset + h.length : hi;
+                if (b > a && nhi - nlo > kChunkBytes) break;
+                if (nhi - nlo > kChunkBytes) { lo = nlo; hi = nhi; b++; break; }  // one oversized record
+                lo = nlo;
+                hi = nhi;
+            }
+            b++;
+        }
+        const uint32_t cn = b - a;
+        if (lo == UINT64_MAX) lo = hi = 0;
+        const uint64_t span = hi - lo;
+        if (span > kChunkBytes) {  // a single record larger than the ring slot: decode it alone, unpipelined
+            for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
+            return -100;  // caller falls back to the whole-batch path
+        }
+        uint8_t *base = reinterpret_cast<uint8_t *>(c->pbuf[slot]);
+        bhg_handle *dh = reinterpret_cast<bhg_handle *>(base + al(kChunkBytes + 64));
+        bhg_desc *dd = reinterpret_cast<bhg_desc *>(reinterpret_cast<uint8_t *>(dh) + al((size_t)max_chunk_n * sizeof(bhg_handle)));
+        uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(dd) +
+                                                                   al((size_t)max_chunk_n * sizeof(bhg_desc)))
+                                    : nullptr;
+        hipStream_t s = c->pstream[slot];
+        // the chunk's handles keep their src-relative offsets: the kernel sees src' = base - lo, src_len' = hi,
+        // and never addresses below base (every in-bounds handle of the chunk has offset >= lo)
+        if (span) HIP_TRY(c, hipMemcpyAsync(base, src + lo, span, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(dh, handles + a, (size_t)cn * sizeof(bhg_handle), hipMemcpyHostToDevice, s));
+        if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc + a, (size_t)cn * 4, hipMemcpyHostToDevice, s));
+        bhg::Launch Ls = L;
+        Ls.stream = s;
+        HIP_TRY(c, bhg::launch_decode_lane(Ls, base - lo, hi, dh, cn, BHG_CODEC_NONE, de, dd, nullptr));
+        HIP_TRY(c, hipMemcpyAsync(out_desc + a, dd, (size_t)cn * sizeof(bhg_desc), hipMemcpyDeviceToHost, s));
+        a = b;
+        slot = (slot + 1) % bhg_ctx::kPipe;
+    }
+    for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
+    return BHG_OK;
+}
+
+}  // namespace
+
 int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
                           int codec, const uint32_t *expected_crc, bhg_desc *out_desc, uint8_t *out_vals,
                           uint64_t out_vals_cap, uint64_t *out_val_off) {
@@ -252,6 +337,14 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     std::lock_guard<std::mutex> g(c->mu);
+    if (codec == BHG_CODEC_NONE && !getenv("BHG_HOST_NOPIPE")) {
+        bool sorted = true;
+        for (uint32_t i = 1; i < n && sorted; i++) sorted = handles[i].offset >= handles[i - 1].offset;
+        if (sorted) {
+            const int r = decode_host_pipelined(c, src, src_len, handles, n, expected_crc, out_desc);
+            if (r != -100) return r;
+        }
+    }
     const size_t hb = (size_t)n * sizeof(bhg_handle), db = (size_t)n * sizeof(bhg_desc);
     const size_t eb = expected_crc ? (size_t)n * 4 : 0, ob = codec == BHG_CODEC_SNAPPY ? ((size_t)n + 1) * 8 : 0;
     const size_t vb = codec == BHG_CODEC_SNAPPY ? (size_t)out_vals_cap : 0;
@@ -283,6 +376,20 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     }
     HIP_TRY(c, hipMemcpyAsync(out_desc, dd, db, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
+    return BHG_OK;
+}
+
+int bhg_host_register(bhg_ctx *c, void *p, uint64_t bytes) {
+    if (!c || !p || !bytes) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return BHG_OK;
+}
+
+int bhg_host_unregister(bhg_ctx *c, void *p) {
+    if (!c || !p) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, hipHostUnregister(p));
     return BHG_OK;
 }
 

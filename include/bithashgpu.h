@@ -141,12 +141,21 @@ int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const b
                      uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                      uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off, void *stream);
 
-/* Same contract with HOST buffers (may be pageable or bhg_malloc_host):
- * copies in, decodes, copies out; synchronous.  This is the end-to-end
- * path (mmap'd .bht -> H2D -> kernel -> D2H). */
+/* Same contract with HOST buffers (may be pageable, bhg_malloc_host or
+ * bhg_host_register'ed): copies in, decodes, copies out; synchronous.  This
+ * is the end-to-end path (mmap'd .bht -> H2D -> kernel -> D2H).  For codec
+ * NONE with handles sorted by offset (table scans, compaction) the batch is
+ * pipelined in <= 64 MiB chunks over 3 streams, so H2D, kernels and D2H
+ * overlap; otherwise src is copied whole first. */
 int bhg_decode_batch_host(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                           uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                           uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off);
+
+/* Page-lock (pin) a caller host range, e.g. an mmap'd .bht file, so the
+ * *_host paths copy it by DMA at the link rate instead of through pageable
+ * staging (hipHostRegister).  Unregister before unmapping. */
+int bhg_host_register(bhg_ctx *ctx, void *p, uint64_t bytes);
+int bhg_host_unregister(bhg_ctx *ctx, void *p);
 
 /* ---- primitives, batched (device) ----
  * crc.New(src[h.offset : h.offset+h.length]).Value() for each handle

@@ -2336,6 +2336,231 @@ __global__ __launch_bounds__(64 * WPB) void k_tile3(const uint8_t *__restrict__ 
     }
 }
 
+
+__device__ __forceinline__ uint32_t zapply4(const uint32_t *Zt, uint32_t c) {
+    return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
+}
+// E11: tile kernel, one window per lane per round, PD rounds of loads in flight
+template <int WPB, int PD, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_tile4(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                          const bhg_handle *__restrict__ handles, uint32_t n,
+                                                          bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Perm::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t Z[5 * 1024];  // Z1024, Z128, Z256, Z512, Z32
+    Crc4Perm::fill(T);
+    for (uint32_t t = threadIdx.x; t < 5 * 1024; t += 64 * WPB) Z[t] = gz[t];
+    __syncthreads();
+    const uint32_t *Z32 = Z + 4096;
+    const Crc4Perm crc(T);
+    const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
+    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
+    bhg_handle hn = {0, 0, 0};
+    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    for (; tile < ntiles; tile += tstride) {
+        // ---------------- phase 1: lane = record (Reader.readData's checks, readRecord, readKV)
+        const bhg_handle h = hn;
+        const uint32_t i = tile * 64 + lane;
+        {
+            const uint32_t tn = tile + tstride;
+            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
+        }
+        const bool valid = i < n;
+        uint32_t st = BHG_ST_OK;
+        bool inb = false;
+        if (valid) {
+            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;                    // reader.go:234-236
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset)
+                st = BHG_ST_INCOMPLETE;                                       // reader.go:251-258
+            else inb = true;
+        }
+        const uint32_t L = inb ? h.length : 0u;
+        const uint64_t p = base + h.offset;
+        const uint32_t m = inb ? (L + 127) / 128 : 1u;
+        const uint32_t hl = L - 128 * (m - 1);
+        uint32_t hw[33];
+        const uint64_t ha = p & ~3ull;
+        const uint32_t hsh = (uint32_t)(p & 3);
+        if (inb) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                if (hl > 60) {
+#pragma unroll
+                    for (int t = 4; t < 8; t++) {
+                        const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                        hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                    }
+                    hw[32] = gld<uint32_t>(ha + 128);
+                } else {
+#pragma unroll
+                    for (int t = 16; t < 33; t++) hw[t] = 0;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        }
+        uint32_t hcrc = 0xffffffffu;  // crc.New: Go's crc32.Update starts from ^0
+        uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
+        uint64_t trailer = 255;       // InternalKeyKindInvalid when ikeySize < 8
+        bool rvalid = false;
+        if (inb) {
+            const uint32_t nw = hl >> 2;
+#pragma unroll
+            for (uint32_t u = 0; u < 32; u++)
+                if (u < nw) hcrc = crc.word(hcrc, __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh));
+            if (hl & 3) {
+                uint32_t wv = 0, wn = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < 32; u++) {
+                    wv = nw == u ? hw[u] : wv;
+                    wn = nw == u ? hw[u + 1] : wn;
+                }
+                hcrc = crc.partial(hcrc, __builtin_amdgcn_alignbyte(wn, wv, hsh), hl & 3);
+            }
+            uint32_t rw[14];
+#pragma unroll
+            for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
+            // readRecordHeader (block2.go:31-36) + readRecord's length check (:57-66)
+            k = L >= 12 ? rw[0] : 0u;
+            v = L >= 12 ? rw[1] : 0u;
+            fn = L >= 12 ? rw[2] : 0u;
+            rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;
+            if (rvalid && k >= 8) {  // readKV / DecodeInternalKey (block2.go:38-55)
+                key_len = k - 8;
+                if (key_len <= 36) {
+                    uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                    for (uint32_t t = 3; t < 12; t++)
+#pragma unroll
+                        for (uint32_t b = 0; b < 4; b++) {
+                            const uint32_t h2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
+                            hh = 4 * (t - 3) + b < key_len ? h2 : hh;
+                        }
+                    fnv = hh;
+                    const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
+                    uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+                    for (uint32_t u = 3; u <= 12; u++) {  // tb <= 48: the trailer ends by byte 56 = rw[13]
+                        a0 = tw == u ? rw[u] : a0;
+                        a1 = tw == u ? rw[u + 1] : a1;
+                        if (u + 2 < 14) a2 = tw == u ? rw[u + 2] : a2;  // tw == 12 only with ts == 0
+                    }
+                    trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
+                              ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
+                } else {
+                    fnv = fnv1_range(p + 12, key_len, end);
+                    trailer = ldu64(p + 12 + k - 8, end);
+                }
+            }
+        }
+        // ---------------- phase 2: 8 rounds, one window per lane per round, PD rounds in flight
+        const bool big = inb && m > 9;  // more than one window per lane: slow path below
+        uint32_t mycrc = 0;
+        constexpr int NB = PD + 1;
+        uint32_t fw[NB][33];
+        uint64_t wa[NB];
+        bool hw_[NB];
+        uint32_t hsel[NB];
+        auto rinfo = [&](uint32_t s, uint64_t &a, bool &has, uint32_t &hs) {
+            const uint32_t sl = 8 * s + rr;
+            const uint32_t Lr = __shfl(L, sl, 64);
+            const uint64_t pr = shfl64(p, sl);
+            const uint32_t mr = __shfl(m, sl, 64);
+            const int32_t q = (int32_t)(mr - 1) - (int32_t)j;  // my window (>= 1)
+            has = Lr != 0 && mr <= 9 && q >= 1;
+            a = pr + (Lr - 128 * (mr - 1)) + 128ull * (uint32_t)(q - 1);
+            hs = (mr <= 9 && j == ((mr - 1) & 7)) ? 1u : 0u;
+        };
+        auto load_win = [&](uint32_t *w, uint64_t a0) {
+            const uint64_t a = a0 & ~3ull;
+            if (MODE & 2) {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = (uint32_t)a * 0x9e3779b9u + t;
+            } else if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+#pragma unroll
+        for (int s0 = 0; s0 < PD; s0++) {
+            rinfo(s0, wa[s0], hw_[s0], hsel[s0]);
+            if (hw_[s0]) load_win(fw[s0], wa[s0]);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int cb = s % NB;
+            if (s + PD < 8) {
+                const int nb = (s + PD) % NB;
+                rinfo(s + PD, wa[nb], hw_[nb], hsel[nb]);
+                if (hw_[nb]) load_win(fw[nb], wa[nb]);
+            }
+            const uint32_t hc = __shfl(hcrc, 8 * s + rr, 64);
+            uint32_t acc = hsel[cb] ? hc : 0u;
+            if (hw_[cb]) {
+                const uint32_t wsh = (uint32_t)(wa[cb] & 3);
+                uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t t = 0; t < 8; t++)
+#pragma unroll
+                    for (uint32_t kk = 0; kk < 4; kk++) {
+                        const uint32_t wi = 8 * kk + t;
+                        const uint32_t wv = __builtin_amdgcn_alignbyte(fw[cb][wi + 1], fw[cb][wi], wsh);
+                        c[kk] = (MODE & 4) ? (((c[kk] << 1) | (c[kk] >> 31)) ^ wv) : crc.word(c[kk], wv);
+                    }
+                uint32_t V = zapply4(Z32, c[0]) ^ c[1];
+                V = zapply4(Z32, V) ^ c[2];
+                V = zapply4(Z32, V) ^ c[3];
+                acc = zapply4(Z, acc) ^ V;
+            }
+            if (j & 1) acc = zapply4(Z + 1024, acc);
+            if (j & 2) acc = zapply4(Z + 2048, acc);
+            if (j & 4) acc = zapply4(Z + 3072, acc);
+            acc ^= __shfl_xor(acc, 1, 64);
+            acc ^= __shfl_xor(acc, 2, 64);
+            acc ^= __shfl_xor(acc, 4, 64);
+            const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);
+            if ((lane >> 3) == (uint32_t)s) mycrc = got;
+        }
+        if (big) mycrc = crc_range_a<8, Crc4Perm, true>(crc, 0xffffffffu, p, L, end);
+        if (valid) {
+            uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
+            uint64_t dtr = 0;
+            if (inb) {
+                dcrc = crc_mask(~mycrc);  // crc.go:31-33
+                if (rvalid) {
+                    dk = 12; dkl = key_len; dvo = 12 + k; dvl = v;  // noCompressor.Decode: zero-copy view
+                    dtr = trailer; dfn = fn; dfnv = fnv;
+                    
+                } else {
+                    dst = BHG_ST_RECORD_NIL;  // ErrBhReadRecordNil
+                }
+            }
+            if (MODE & 16) { if (dcrc == 0x12345678u) reinterpret_cast<uint32_t *>(out)[lane] = dfnv; continue; }
+            uint2 *o = reinterpret_cast<uint2 *>(out + i);
+            o[0] = make_uint2(dk, dkl);
+            o[1] = make_uint2(dvo, dvl);
+            o[2] = make_uint2((uint32_t)dtr, (uint32_t)(dtr >> 32));
+            o[3] = make_uint2(dfn, dfnv);
+            o[4] = make_uint2(dcrc, dst);
+        }
+    }
+}
+
+
 // ============================================================== launchers
 static int g_cus = 256;
 constexpr uint32_t kLabShiftSets = 3;  // CH = 64, 128, 256
@@ -2529,12 +2754,27 @@ static void L_tile3(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_
     hipLaunchKernelGGL((k_tile3<WPB, Tab, MODE, PD>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
 }
 
+template <int WPB, int PD, int MODE, int WPC = 1>
+static void L_tile4(const uint8_t *s, uint64_t len, const bhg_handle *h, uint32_t n, bhg_desc *o, const uint32_t *tabs,
+                    hipStream_t st) {
+    const uint32_t nt = (n + 63) / 64;
+    uint32_t grid = std::min<uint32_t>((nt + WPB - 1) / WPB, g_cus * WPC);
+    hipLaunchKernelGGL((k_tile4<WPB, PD, MODE>), dim3(grid), dim3(64 * WPB), 0, st, s, len, h, n, o, tabs + kLabWinOff);
+}
+
 struct LabEntry {
     const char *name;
     launch_fn fn;
     bool diag;
 };
 static const LabEntry kLab[] = {
+    {"tile4_w8_pd1", L_tile4<8, 1, 0>, false},
+    {"tile4_w8_pd2", L_tile4<8, 2, 0>, false},
+    {"tile4_w8_pd3", L_tile4<8, 3, 0>, false},
+    {"tile4_w8_pd2_loads", L_tile4<8, 2, 4>, true},
+    {"tile4_w8_pd3_loads", L_tile4<8, 3, 4>, true},
+    {"tile4_w8_pd2_nod", L_tile4<8, 2, 16>, true},
+    {"tile4_w8_pd2_compute", L_tile4<8, 2, 2>, true},
     {"tile3_w8_pd2", L_tile3<8, Crc4Perm, 0, 2>, false},
     {"tile3_w8_pd3", L_tile3<8, Crc4Perm, 0, 3>, false},
     {"tile3_w8_pd1", L_tile3<8, Crc4Perm, 0, 1>, false},

@@ -310,3 +310,45 @@ def test_snappy_kernel_variants(sv, monkeypatch):
     assert_desc_equal(got, exp)
     assert np.array_equal(go, eo) and gv.tobytes() == ev[:int(eo[-1])].tobytes()
     c.close()
+
+
+@pytest.mark.parametrize("chunk,big", [(4096, False), (1 << 20, False), (4096, True)])
+def test_host_pipelined_sorted(chunk, big, monkeypatch):
+    """bhg_decode_batch_host, NoCompressor, handles sorted by offset: the
+    chunked 3-stream pipeline (tiny chunks force many chunks, records larger
+    than a chunk force the whole-batch fallback) equals the restatement,
+    including zero-length / out-of-range handles and expected_crc."""
+    from bitalosdb_amd.codec import BithashCodec
+    monkeypatch.setenv("BHG_HOST_CHUNK_BYTES", str(chunk))
+    c = BithashCodec(0)
+    rng = random.Random(chunk)
+    sizes = [1, 64, 1024, 3000] + ([9000] if big else [])
+    specs = [(rand_bytes(rng, rng.choice([0, 7, 32, 40])), rand_bytes(rng, rng.choice(sizes)), 9)
+             for _ in range(3000)]
+    src, h = make_records(rng, specs, gap_max=5)
+    h = h.copy()
+    h["length"][100] = 0                       # ErrBhIllegalBlockLength
+    h["length"][2999] += 7                     # runs past src: INCOMPLETE
+    exp, _, _ = O.decode_batch(src, h)
+    expected = exp["crc"].copy()
+    expected[5::97] ^= 1
+    got, _, _ = c.decode_host(np.frombuffer(src, np.uint8).copy(), h, expected_crc=expected)
+    exp2, _, _ = O.decode_batch(src, h, expected_crc=expected)
+    assert_desc_equal(got, exp2)
+    assert (got["status"] == 6).sum() > 0
+    c.close()
+
+
+def test_host_pipelined_registered(codec):
+    """Pinned (bhg_host_register) host source through the pipelined path."""
+    rng = random.Random(77)
+    specs = [(rand_bytes(rng, 32), rand_bytes(rng, 1024), 3) for _ in range(4000)]
+    src, h = make_records(rng, specs)
+    buf = np.frombuffer(src, np.uint8).copy()
+    codec.host_register(buf)
+    try:
+        got, _, _ = codec.decode_host(buf, h)
+    finally:
+        codec.host_unregister(buf)
+    exp, _, _ = O.decode_batch(src, h)
+    assert_desc_equal(got, exp)
