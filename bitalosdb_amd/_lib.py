@@ -23,14 +23,16 @@ assert HANDLE_DT.itemsize == 16 and DESC_DT.itemsize == 40
 BHG_OK, BHG_EINVAL, BHG_EHIP, BHG_ENOMEM, BHG_ENODEV, BHG_ECAPACITY = 0, -1, -2, -3, -4, -5
 CODEC_NONE, CODEC_SNAPPY = 0, 1
 ST_OK, ST_RECORD_NIL, ST_ILLEGAL_LENGTH, ST_INCOMPLETE, ST_SNAPPY_CORRUPT, ST_SNAPPY_TOO_LARGE, \
-    ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED = range(10)
+    ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED, ST_NOT_FOUND = range(11)
+TABLE_DT = np.dtype([("base", "<u8"), ("index_off", "<u8"), ("index_len", "<u8"), ("conflict_off", "<u8"),
+                     ("conflict_bh_off", "<u4"), ("conflict_bh_len", "<u4")])
 
 EXPORTS = [
     "bhg_abi_version", "bhg_device_count", "bhg_create", "bhg_destroy", "bhg_last_error", "bhg_stream",
     "bhg_stream_sync", "bhg_malloc_device", "bhg_free_device", "bhg_malloc_host", "bhg_free_host",
     "bhg_memcpy_h2d", "bhg_memcpy_d2h", "bhg_memset_device", "bhg_decode_batch", "bhg_decode_batch_host",
     "bhg_crc32c_masked_batch", "bhg_fnv32_batch", "bhg_encode_batch", "bhg_scan_tables",
-    "bhg_host_register", "bhg_host_unregister",
+    "bhg_host_register", "bhg_host_unregister", "bhg_get_batch",
 ]
 
 
@@ -85,6 +87,7 @@ def lib():
             "bhg_scan_tables": (I, [P, P, P, U32, I, P, U64, P, P, P]),
             "bhg_host_register": (I, [P, P, U64]),
             "bhg_host_unregister": (I, [P, P]),
+            "bhg_get_batch": (I, [P, P, U64, P, U32, P, P, P, P, U32, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -183,6 +183,76 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_decode_batch_host")
         return desc, (None if vals is None else vals[:int(off[-1])]), off
 
+    def get_batch(self, src_t, tables, keys, table_idx, khash=None):
+        """Batched Reader.Get index path (bhg_get_batch): returns device tensors
+        (handles [n] as int64 pairs in HANDLE_DT layout, status [n] int32).
+
+        src_t: device uint8 tensor holding the table files; tables: TABLE_DT
+        array (bitalosdb_amd.table.open_table records); keys: list of user
+        keys or (bytes, key_off[n+1]); table_idx: per query."""
+        if isinstance(keys, tuple):
+            kb, ko = keys
+        else:
+            ko = np.zeros(len(keys) + 1, dtype=np.uint64)
+            ko[1:] = np.cumsum([len(k) for k in keys])
+            kb = b"".join(bytes(k) for k in keys)
+        n = len(ko) - 1
+        dev = self.device
+        with torch.cuda.stream(self.stream):
+            tab_t = torch.from_numpy(np.ascontiguousarray(tables, dtype=B.TABLE_DT).view(np.uint8).copy()).to(dev)
+            kb_t = torch.from_numpy(np.frombuffer(kb, np.uint8).copy() if len(kb) else np.zeros(1, np.uint8)).to(dev)
+            ko_t = torch.from_numpy(np.ascontiguousarray(ko, dtype=np.uint64).view(np.int64)).to(dev)
+            ti_t = torch.from_numpy(np.ascontiguousarray(table_idx, dtype=np.uint32).view(np.int32)).to(dev)
+            kh_t = None if khash is None else torch.from_numpy(
+                np.ascontiguousarray(khash, dtype=np.uint32).view(np.int32)).to(dev)
+            out_h = torch.empty(max(n, 1) * 2, dtype=torch.int64, device=dev)
+            out_s = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        self.get_batch_dev(src_t, tab_t, len(tables), kb_t, ko_t, ti_t, kh_t, n, out_h, out_s)
+        return out_h[:2 * n], out_s[:n]
+
+    def get_batch_dev(self, src_t, tab_t, ntables, kb_t, ko_t, ti_t, kh_t, n, out_h, out_s):
+        """bhg_get_batch on device-resident inputs (no copies)."""
+        rc = self.L.bhg_get_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(tab_t), ntables, _ptr(kb_t),
+                                  _ptr(ko_t), _ptr(ti_t), _ptr(kh_t), n, _ptr(out_h), _ptr(out_s), self._stream())
+        B.check(self.ctx, rc, "bhg_get_batch")
+
+    def crc_masked_bytes(self, b):
+        """crc.New(b).Value() of one host byte string, on the GPU (bhg_crc32c_masked_batch)."""
+        with torch.cuda.stream(self.stream):
+            t = torch.from_numpy(np.frombuffer(bytes(b), np.uint8).copy() if len(b) else np.zeros(1, np.uint8))
+            t = t.to(self.device)
+            h = np.zeros(1, dtype=HANDLE_DT)
+            h["length"] = len(b)
+            ht = handles_tensor(h, self.device)
+            out = self.crc_batch(t, ht, 1)
+            self.sync()
+        return int(out.cpu().numpy().view(np.uint32)[0])
+
+    def multi_get(self, src_t, tables, keys, table_idx, compressor=NoCompressor):
+        """Bithash.Get over a batch: index lookup, then readData of the found
+        handles (bhg_decode_batch).  Returns (status per query, desc, vals, val_off)
+        as numpy; status BHG_ST_* with NOT_FOUND / ILLEGAL_LENGTH from the index
+        path and the decode status otherwise."""
+        with torch.cuda.stream(self.stream):
+            h_t, s_t = self.get_batch(src_t, tables, keys, table_idx)
+            n = s_t.numel()
+            vals = None
+            if compressor == SnappyCompressor:
+                probe = self.decode_batch(src_t, src_t.numel(), h_t, n, compressor)
+                self.sync()
+                total = int(probe.val_off_np()[-1]) if n else 0
+                vals = torch.zeros(max(total, 1), dtype=torch.uint8, device=self.device)
+            res = self.decode_batch(src_t, src_t.numel(), h_t, n, compressor=compressor, out_vals=vals)
+            self.sync()
+        st = s_t.cpu().numpy().view(np.uint32).copy()
+        desc = res.desc_np()
+        ok = st == B.ST_OK
+        st[ok] = desc["status"][ok]
+        if compressor == SnappyCompressor:
+            off = res.val_off_np()
+            return st, desc, vals.cpu().numpy()[:int(off[-1])], off
+        return st, desc, None, None
+
     def host_register(self, arr):
         """Pin a host numpy buffer (bhg_host_register) for DMA-rate *_host copies."""
         B.check(self.ctx, self.L.bhg_host_register(self.ctx, _ptr(arr), arr.nbytes), "bhg_host_register")

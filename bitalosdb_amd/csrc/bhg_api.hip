@@ -379,6 +379,21 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     return BHG_OK;
 }
 
+int bhg_get_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_table *tables, uint32_t ntables,
+                  const uint8_t *keys, const uint64_t *key_off, const uint32_t *table_idx, const uint32_t *khash,
+                  uint32_t n, bhg_handle *out_handles, uint32_t *out_status, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (n == 0) return BHG_OK;
+    if (!tables || !key_off || !table_idx || !out_handles || !out_status || (!src && src_len) || !keys) {
+        set_err(c, "null buffer");
+        return BHG_EINVAL;
+    }
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, bhg::launch_get(launch_of(c, stream), src, src_len, tables, ntables, keys, key_off, table_idx, khash, n,
+                               out_handles, out_status));
+    return BHG_OK;
+}
+
 int bhg_host_register(bhg_ctx *c, void *p, uint64_t bytes) {
     if (!c || !p || !bytes) return BHG_EINVAL;
     if (int r = set_device(c)) return r;

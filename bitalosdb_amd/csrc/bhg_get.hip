@@ -1,0 +1,237 @@
+// bhg_get.hip -- batched point lookup over .bht tables resident in HBM.
+//
+// k_get: one LANE per query.  Reader.Get minus the pread (bithash/reader.go:209-231):
+//   khash   = hash.Fnv32(key)                                (internal/hash/fnv.go:19-23)
+//   v, ok   = HashIndex.Get64(khash)                         (internal/bindex/hash_index.go:399-431)
+//             shard counts and items are BIG-endian; items are {u16 lo16, u64 value} sorted by lo16
+//             within the shard; findItem is a lower-bound binary search   (:487-503)
+//   bh      = decodeBlockHandle(LE bytes of v)               (reader.go:215-217)
+//   if conflictBH.Length != 0 && bh.Offset >= conflictBH.Offset && bh.Length <= conflictBH.Length:
+//       bh = readConflict(key): blockIter.SeekGE over the conflict block  (reader.go:274-289,
+//            block.go:274-350): binary search over the restart points, then a forward scan
+//            of prefix-compressed entries (block.go:112-182); hit iff the entry's UserKey == key
+//       miss -> {0, 0} -> ErrBhIllegalBlockLength (reader.go:224-226)
+// The output handle is rebased to src (table base + bh.Offset) so that it can
+// be fed straight to bhg_decode_batch: Get + readData as two launches.
+//
+// Lookups are latency-bound dependent reads (2 shard counts + log2(items in
+// the shard) item probes, ~1.5 MB of index per table: L2/MALL-resident under
+// load); the grid is sized for many queries in flight per CU.
+#include "bhg_device.h"
+#include "bhg_internal.h"
+
+namespace bhg {
+
+namespace {
+
+__device__ __forceinline__ uint32_t ld8(uint64_t a) { return gld<uint8_t>(a); }
+__device__ __forceinline__ uint32_t be16(uint64_t a) { return (ld8(a) << 8) | ld8(a + 1); }
+__device__ __forceinline__ uint32_t be32(uint64_t a) {
+    return (ld8(a) << 24) | (ld8(a + 1) << 16) | (ld8(a + 2) << 8) | ld8(a + 3);
+}
+__device__ __forceinline__ uint64_t be64(uint64_t a) { return ((uint64_t)be32(a) << 32) | be32(a + 4); }
+__device__ __forceinline__ uint32_t le32(uint64_t a) {
+    return ld8(a) | (ld8(a + 1) << 8) | (ld8(a + 2) << 16) | (ld8(a + 3) << 24);
+}
+
+// readEntry's varint32 (block.go:115-172): up to 5 bytes, the 5th taken whole
+__device__ __forceinline__ uint32_t uvarint32(uint64_t &p) {
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t b = ld8(p + i);
+        if (b < 128 || i == 4) {
+            x |= b << (7 * i);
+            p += i + 1;
+            return x;
+        }
+        x |= (b & 0x7fu) << (7 * i);
+    }
+    return x;
+}
+
+// bytes.Compare(a[0:al], b[0:bl]) over device memory
+__device__ __forceinline__ int bcmp(uint64_t a, uint32_t al, uint64_t b, uint32_t bl) {
+    const uint32_t m = al < bl ? al : bl;
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t x = ld8(a + i), y = ld8(b + i);
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+constexpr uint32_t kShards = 65536;          // HashIndexShardsNum
+constexpr uint32_t kHdr = 8;                 // SuccinctHeaderSize
+constexpr uint32_t kItemOff = kHdr + kShards * 4;
+constexpr uint32_t kItem = 10;               // HashIndexItem64Size
+constexpr uint64_t kSearchTrailer = ((1ull << 56) - 1) << 8 | 18;  // MakeSearchKey: SeqNumMax, KindMax
+
+// HashIndex.Get64 (hash_index.go:399-431); false = not found
+__device__ bool get64(uint64_t d, uint64_t len, uint32_t key, uint64_t &val) {
+    if (len <= kItemOff) return false;        // SetReader rejects len(d) <= itemOffset
+    if (be32(d + 4) == 0) return false;       // header.shards <= 0
+    const uint32_t hid = key >> 16, lid = key & 0xffffu;
+    const uint32_t origin = hid > 0 ? be32(d + kHdr + (hid - 1) * 4) : 0u;
+    const uint32_t dest = be32(d + kHdr + hid * 4);
+    if (dest <= origin) return false;
+    const uint32_t cnt = dest - origin;
+    const uint64_t cur = d + kItemOff + (uint64_t)origin * kItem;
+    if ((uint64_t)kItemOff + ((uint64_t)origin + cnt) * kItem > len) return false;  // corrupt index: Go would panic
+    uint32_t i = 0, j = cnt;
+    while (i < j) {
+        const uint32_t h = (i + j) >> 1;
+        if (be16(cur + (uint64_t)kItem * h) < lid) i = h + 1;
+        else j = h;
+    }
+    if (i < cnt && be16(cur + (uint64_t)kItem * i) == lid) {
+        val = be64(cur + (uint64_t)kItem * i + 2);
+        return true;
+    }
+    return false;
+}
+
+// readConflict (reader.go:274-289): SeekGE(key) then UserKey == key; returns the
+// entry's 8-B block handle or {0, 0}.  Keys are InternalKeys; the search key is
+// MakeSearchKey(key) = (key, SeqNumMax, KindMax), ordered by InternalCompare
+// (internal.go:108-119): UserKey ascending, then trailer descending.
+constexpr uint32_t kMaxChain = 32;  // entries per restart interval (the writer uses 16, block.go:607)
+
+struct Chain {  // the entries since the last restart: full key of entry e = key(e-1)[:sh[e]] || suffix(e)
+    uint32_t n;
+    uint32_t sh[kMaxChain];
+    uint64_t sa[kMaxChain];
+    __device__ uint32_t byte_at(uint32_t e, uint32_t idx) const {
+        while (idx < sh[e]) e--;  // sh[0] == 0 at the restart: terminates
+        return ld8(sa[e] + (idx - sh[e]));
+    }
+};
+
+// sign of InternalCompare(search key, entry e's key of length kl)
+__device__ int cmp_search(const Chain &C, uint32_t e, uint32_t kl, uint64_t key, uint32_t klen) {
+    const uint32_t ul = kl >= 8 ? kl - 8 : 0u;  // kl < 8: UserKey nil, trailer Invalid (255)
+    const uint32_t m = klen < ul ? klen : ul;
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t x = ld8(key + i), y = C.byte_at(e, i);
+        if (x != y) return x < y ? -1 : 1;
+    }
+    if (klen != ul) return klen < ul ? -1 : 1;
+    uint64_t tr = 255;
+    if (kl >= 8) {
+        tr = 0;
+        for (uint32_t b = 0; b < 8; b++) tr |= (uint64_t)C.byte_at(e, ul + b) << (8 * b);
+    }
+    return kSearchTrailer > tr ? -1 : (kSearchTrailer < tr ? 1 : 0);
+}
+
+__device__ void seek_conflict(uint64_t blk, uint32_t blen, uint64_t key, uint32_t klen, uint32_t &off,
+                              uint32_t &length) {
+    off = 0;
+    length = 0;
+    if (blen < 4) return;
+    const uint32_t nres = le32(blk + blen - 4);
+    if (nres == 0 || (uint64_t)4 * (nres + 1) > blen) return;  // newBlockIter: no restart points
+    const uint64_t restarts = blk + blen - 4ull * (nres + 1);
+    const uint32_t data_end = blen - 4 * (nres + 1);
+    Chain C;
+    // binary search over the restart points (block.go:281-333); a restart key is stored whole
+    uint32_t index = 0, upper = nres;
+    while (index < upper) {
+        const uint32_t h = (index + upper) >> 1;
+        uint64_t p = blk + le32(restarts + 4ull * h) + 1;  // skip shared (== 0, one byte)
+        const uint32_t un = uvarint32(p);
+        (void)uvarint32(p);
+        C.n = 1;
+        C.sh[0] = 0;
+        C.sa[0] = p;
+        if (cmp_search(C, 0, un, key, klen) >= 0) index = h + 1;
+        else upper = h;
+    }
+    uint32_t o = index > 0 ? le32(restarts + 4ull * (index - 1)) : 0u;
+    // forward scan (readEntry + Next) until the first entry >= search key
+    C.n = 0;
+    while (o < data_end) {
+        uint64_t p = blk + o;
+        const uint32_t sh = uvarint32(p), un = uvarint32(p), vl = uvarint32(p);
+        if (sh == 0) C.n = 0;
+        if (C.n == kMaxChain) return;  // longer restart interval than any writer of this format emits
+        C.sh[C.n] = sh;
+        C.sa[C.n] = p;
+        const uint32_t e = C.n++;
+        const uint32_t kl = sh + un;
+        if (cmp_search(C, e, kl, key, klen) <= 0) {  // entry >= search key
+            // hit iff UserKey == key (bytes.Equal): same length and bytes
+            if (kl >= 8 && kl - 8 == klen) {
+                bool eq = true;
+                for (uint32_t i = 0; i < klen && eq; i++) eq = ld8(key + i) == C.byte_at(e, i);
+                if (eq && vl >= 8) {  // decodeBlockHandle (block.go:26-39)
+                    off = le32(p + un);
+                    length = le32(p + un + 4);
+                }
+            }
+            return;
+        }
+        o = (uint32_t)(p + un + vl - blk);
+    }
+}
+
+template <bool HAVE_HASH>
+__global__ __launch_bounds__(256) void k_get(const uint8_t *__restrict__ src, uint64_t src_len,
+                                             const bhg_table *__restrict__ tables, uint32_t ntables,
+                                             const uint8_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
+                                             const uint32_t *__restrict__ table_idx, const uint32_t *__restrict__ khash,
+                                             uint32_t n, bhg_handle *__restrict__ out_h, uint32_t *__restrict__ out_st) {
+    const uint64_t base = (uint64_t)src;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t ti = table_idx[i];
+        const uint64_t k0 = key_off[i], k1 = key_off[i + 1];
+        const uint64_t kp = (uint64_t)keys + k0;
+        const uint32_t klen = (uint32_t)(k1 - k0);
+        bhg_handle h = {0, 0, 0};
+        uint32_t st = BHG_ST_NOT_FOUND;
+        if (ti < ntables) {
+            const bhg_table t = tables[ti];
+            uint32_t kh;
+            if (HAVE_HASH) {
+                kh = khash[i];
+            } else {
+                kh = BHG_FNV_OFFSET;
+                for (uint32_t b = 0; b < klen; b++) kh = (kh * BHG_FNV_PRIME) ^ ld8(kp + b);
+            }
+            uint64_t v;
+            const bool idx_ok = t.index_off <= src_len && t.index_len <= src_len - t.index_off;
+            if (idx_ok && get64(base + t.index_off, t.index_len, kh, v)) {
+                uint32_t bo = (uint32_t)v, bl = (uint32_t)(v >> 32);  // LE handle bytes (reader.go:215-217)
+                st = BHG_ST_OK;
+                if (t.conflict_bh_len != 0 && bo >= t.conflict_bh_off && bl <= t.conflict_bh_len) {
+                    const bool cf_ok = t.conflict_off <= src_len && t.conflict_bh_len <= src_len - t.conflict_off;
+                    if (cf_ok) seek_conflict(base + t.conflict_off, t.conflict_bh_len, kp, klen, bo, bl);
+                    else bo = bl = 0;
+                    if (bo == 0 && bl == 0) st = BHG_ST_ILLEGAL_LENGTH;  // reader.go:224-226
+                }
+                if (st == BHG_ST_OK) h = bhg_handle{t.base + bo, bl, 0};
+            }
+        }
+        out_h[i] = h;
+        out_st[i] = st;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_get(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_table *tables, uint32_t ntables,
+                      const uint8_t *keys, const uint64_t *key_off, const uint32_t *table_idx, const uint32_t *khash,
+                      uint32_t n, bhg_handle *out_h, uint32_t *out_st) {
+    uint64_t need = (n + 255) / 256;
+    uint64_t cap = (uint64_t)L.num_cus * 16;
+    uint32_t grid = (uint32_t)(need < cap ? need : cap);
+    if (grid == 0) grid = 1;
+    if (khash)
+        hipLaunchKernelGGL(k_get<true>, dim3(grid), dim3(256), 0, L.stream, src, src_len, tables, ntables, keys,
+                           key_off, table_idx, khash, n, out_h, out_st);
+    else
+        hipLaunchKernelGGL(k_get<false>, dim3(grid), dim3(256), 0, L.stream, src, src_len, tables, ntables, keys,
+                           key_off, table_idx, khash, n, out_h, out_st);
+    return hipGetLastError();
+}
+
+}  // namespace bhg

@@ -40,6 +40,11 @@ hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_l
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 
+// bhg_get.hip
+hipError_t launch_get(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_table *tables, uint32_t ntables,
+                      const uint8_t *keys, const uint64_t *key_off, const uint32_t *table_idx, const uint32_t *khash,
+                      uint32_t n, bhg_handle *out_h, uint32_t *out_st);
+
 // bhg_encode.hip
 struct EncodeLaunch {
     const uint8_t *keys;

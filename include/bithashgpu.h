@@ -62,6 +62,7 @@ extern "C" {
 #define BHG_ST_KEY_TOO_LARGE 7     /* ErrBhKeyTooLarge  (writer.go:260-261) */
 #define BHG_ST_VALUE_TOO_LARGE 8   /* ErrBhValueTooLarge (writer.go:262-263) */
 #define BHG_ST_DATA_MAX_EXCEEDED 9 /* "bithash: panic add exceed data max size" (writer.go:266-269) */
+#define BHG_ST_NOT_FOUND 10        /* HashIndex miss: ErrBhNotFound (reader.go:210-213) */
 
 /* BlockHandle (block.go:26-39) with the offset widened to 64 bits so one
  * batch may span many concatenated/mmap'd table files. 16 B. */
@@ -210,6 +211,36 @@ int bhg_encode_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key_off,
 int bhg_scan_tables(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                     bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
                     void *stream);
+
+/* ---- batched point lookup (device): Reader.Get minus the pread ----
+ * One opened table (NewReader, bithash/reader.go:73-183, done by the host):
+ *   base            : byte offset of the table file inside src
+ *   index_off/len   : the HashIndex bytes (the indexhash_data value of the
+ *                     indexhash block), offset inside src; len 0 = no keys
+ *   conflict_off    : offset inside src of the conflict block
+ *   conflict_bh_*   : conflictBH as read from the meta block (table-relative;
+ *                     length 0 = no conflict block)                       40 B */
+typedef struct bhg_table {
+    uint64_t base;
+    uint64_t index_off;
+    uint64_t index_len;
+    uint64_t conflict_off;
+    uint32_t conflict_bh_off;
+    uint32_t conflict_bh_len;
+} bhg_table;
+
+/* For each query i (UserKey keys[key_off[i] : key_off[i+1]] in table
+ * tables[table_idx[i]]): khash = hash.Fnv32(key) unless khash[] is given,
+ * HashIndex.Get64 (internal/bindex/hash_index.go:399-431), and for handles in
+ * the conflict range the conflict block SeekGE (reader.go:218-228, 274-289;
+ * block.go:274-350).  Writes out_handles[i] = {table base + bh.Offset,
+ * bh.Length} (feed to bhg_decode_batch for readData) and out_status[i] =
+ * BHG_ST_OK, BHG_ST_NOT_FOUND (ErrBhNotFound) or BHG_ST_ILLEGAL_LENGTH
+ * (conflict miss -> ErrBhIllegalBlockLength).  Replaces Reader.Get /
+ * Bithash.Get's index path (bithash.go:101-119).  All pointers device. */
+int bhg_get_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_table *tables, uint32_t ntables,
+                  const uint8_t *keys, const uint64_t *key_off, const uint32_t *table_idx, const uint32_t *khash,
+                  uint32_t n, bhg_handle *out_handles, uint32_t *out_status, void *stream);
 
 #ifdef __cplusplus
 }

@@ -463,6 +463,23 @@ def table_get(f, ukey, compressor=0):
     return _read_data(f, (off, length), compressor)
 
 
+def get_handle(f, ukey):
+    """Reader.Get's index path (reader.go:209-231) without readData:
+    returns (status, bh_off, bh_len) with status "OK", "NOT_FOUND" or "ILLEGAL_LENGTH"."""
+    t = open_table(f)
+    v = hash_index_get64(t["index_data"], O.fnv32(ukey))
+    if v is None:
+        return "NOT_FOUND", 0, 0
+    off, length = v & 0xFFFFFFFF, v >> 32
+    coff, clen = t["conflict_bh"]
+    if clen != 0 and off >= coff and length <= clen:
+        uk, cv = block_seek_ge(t["conflict_buf"], bytes(ukey))
+        off, length = decode_bh(cv) if cv is not None and uk == bytes(ukey) else (0, 0)
+        if (off, length) == (0, 0):
+            return "ILLEGAL_LENGTH", 0, 0
+    return "OK", off, length
+
+
 def _read_data(f, bh, compressor):
     """Reader.readData (reader.go:233-272) for one handle."""
     off, length = bh

@@ -25,6 +25,9 @@ for s in $STEPS; do
       cat $OUT/bench_scan.log
       timeout -k 10 300 python bench.py --config scanmix --steps 10 --warmup 2 > $OUT/bench_scanmix.log 2>&1 || exit $?
       cat $OUT/bench_scanmix.log ;;
+    get)
+      timeout -k 10 600 python bench.py --config get --steps 10 --warmup 2 > $OUT/bench_get.log 2>&1 || exit $?
+      cat $OUT/bench_get.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
       cat $OUT/smoke.log ;;

@@ -1,0 +1,164 @@
+"""GPU parity: batched Reader.Get (bhg_get_batch: FNV-1 -> HashIndex.Get64 ->
+conflict-block SeekGE) and Bithash.Get over a batch (get + readData) vs the
+restatement (oracle/table.py get_handle / table_get).
+
+Tables: the K2 known-answer table (6 FNV-1 collision pairs -> conflict block,
+bithash_test.go:643-723), writer-built tables with overwrites, snappy values,
+an empty table, and hash-colliding keys that were never written (they hit the
+conflict range and miss in SeekGE -> ErrBhIllegalBlockLength)."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from bitalosdb_amd import table as BT
+from bitalosdb_amd._lib import ST_ILLEGAL_LENGTH, ST_NOT_FOUND, ST_OK
+from oracle import oracle as O
+from oracle import table as T
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ST = {"OK": ST_OK, "NOT_FOUND": ST_NOT_FOUND, "ILLEGAL_LENGTH": ST_ILLEGAL_LENGTH}
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from bitalosdb_amd import _lib
+    from bitalosdb_amd.codec import BithashCodec
+    _lib.lib()
+    c = BithashCodec(0)
+    yield c
+    c.close()
+
+
+def _writer_table(rng, n, fn, compressor=0, dup=0.1, keys=None):
+    w = T.Writer(fn, 1 << 30, compressor=compressor)
+    written = []
+    for i in range(n):
+        if keys is not None:
+            k = keys[i]
+        elif written and rng.random() < dup:
+            k = rng.choice(written)
+        else:
+            k = bytes(rng.randrange(97, 123) for _ in range(rng.choice([3, 16, 32])))
+        v = bytes(rng.randrange(65, 91) for _ in range(rng.choice([1, 50, 700])))
+        w.add(k, ((i + 1) << 8) | 1, v)
+        written.append(k)
+    w.write_table(True)
+    return bytes(w.file), written
+
+
+def _k2_keys():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("kat", os.path.join(os.path.dirname(__file__),
+                                                                      "test_oracle_known_answers.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return list(m.K2_KEYS)
+
+
+def _concat(files):
+    src = bytearray()
+    recs = []
+    for f in files:
+        base = len(src) + 5                # odd padding between tables: bases need no alignment
+        src += bytes(5) + f
+        rec, _ = BT.open_table(f, base=base)
+        recs.append(rec)
+    return bytes(src), np.array(recs, dtype=recs[0].dtype)
+
+
+def _check(codec, files, queries):
+    src, tabs = _concat(files)
+    src_t = torch.from_numpy(np.frombuffer(src, np.uint8).copy()).to(codec.device)
+    keys = [q[1] for q in queries]
+    tidx = np.array([q[0] for q in queries], dtype=np.uint32)
+    h_t, s_t = codec.get_batch(src_t, tabs, keys, tidx)
+    codec.sync()
+    h = h_t.cpu().numpy().view(np.uint8).view(O.HANDLE_DT)
+    st = s_t.cpu().numpy().view(np.uint32)
+    for i, (t, k) in enumerate(queries):
+        es, eo, el = T.get_handle(files[t], k)
+        assert st[i] == ST[es], (i, k, es, st[i])
+        if es == "OK":
+            assert int(h["offset"][i]) == int(tabs["base"][t]) + eo and int(h["length"][i]) == el, (i, k)
+    return src_t, tabs, keys, tidx
+
+
+def test_get_k2_conflict_table(codec):
+    b = open(os.path.join(GOLD, "k2.bht"), "rb").read()
+    keys2 = _k2_keys()
+    t = T.open_table(b)
+    all_keys = [uk for uk, _, _, _ in T.table_iter(b)]
+    rng = random.Random(5)
+    missing = [bytes(rng.randrange(97, 123) for _ in range(20)) for _ in range(200)]
+    qs = [(0, k) for k in all_keys + keys2 + missing]
+    _check(codec, [b], qs)
+    assert t["conflict_bh"][1] > 0
+
+
+def test_get_conflict_range_miss(codec):
+    """A key whose FNV-1 equals a conflicting hash but was never written:
+    HashIndex hit on conflictBH, SeekGE miss -> ILLEGAL_LENGTH."""
+    keys2 = _k2_keys()
+    f, _ = _writer_table(random.Random(1), 3, 9, keys=[keys2[0], keys2[1], b"solo"])
+    # keys2[0], keys2[1] collide; build a third collider of the same pair by reusing the hash via a table of
+    # only keys2[0] and looking up keys2[1] in a table where keys2[0] collides with another written key
+    qs = [(0, keys2[0]), (0, keys2[1]), (0, b"solo"), (0, b"absent")]
+    _check(codec, [f], qs)
+    f2, _ = _writer_table(random.Random(2), 3, 9, keys=[keys2[0], keys2[1], keys2[2]])
+    # keys2[3] pairs with keys2[2]: its hash is in the index as a plain (non-conflict) entry -> OK with keys2[2]'s
+    # handle (Reader.Get does not compare keys outside the conflict block, reader.go:209-231)
+    _check(codec, [f2], [(0, k) for k in keys2[:6]])
+
+
+@pytest.mark.parametrize("compressor", [0, 1])
+def test_multi_table_multiget(codec, compressor):
+    rng = random.Random(10 + compressor)
+    files, written = [], []
+    for t in range(3):
+        f, w = _writer_table(rng, 400, 20 + t, compressor=compressor)
+        files.append(f)
+        written.append(w)
+    empty, _ = _writer_table(rng, 0, 30)
+    files.append(empty)
+    qs = []
+    for _ in range(3000):
+        t = rng.randrange(4)
+        if t < 3 and rng.random() < 0.8:
+            qs.append((t, rng.choice(written[t])))
+        else:
+            qs.append((t, bytes(rng.randrange(97, 123) for _ in range(rng.choice([3, 16, 32])))))
+    src_t, tabs, keys, tidx = _check(codec, files, qs)
+    st, desc, vals, voff = codec.multi_get(src_t, tabs, keys, tidx, compressor=compressor)
+    for i, (t, k) in enumerate(qs):
+        try:
+            exp = T.table_get(files[t], k, compressor)
+        except T.BithashError as e:
+            assert st[i] != ST_OK, (i, str(e))
+            continue
+        assert st[i] == ST_OK
+        if compressor:
+            got = vals[int(voff[i]):int(voff[i + 1])].tobytes()
+        else:
+            off = int(tabs["base"][t])
+            hoff = int(T.get_handle(files[t], k)[1])
+            got = bytes(files[t][hoff + int(desc["val_off"][i]):hoff + int(desc["val_off"][i]) + int(desc["val_len"][i])])
+            assert off >= 0
+        assert got == exp, i
+
+
+def test_given_khash_matches(codec):
+    rng = random.Random(3)
+    f, w = _writer_table(rng, 300, 4)
+    src, tabs = _concat([f])
+    src_t = torch.from_numpy(np.frombuffer(src, np.uint8).copy()).to(codec.device)
+    keys = w[:200]
+    kh = np.array([O.fnv32(k) for k in keys], dtype=np.uint32)
+    h1, s1 = codec.get_batch(src_t, tabs, keys, np.zeros(200, np.uint32))
+    h2, s2 = codec.get_batch(src_t, tabs, keys, np.zeros(200, np.uint32), khash=kh)
+    codec.sync()
+    assert torch.equal(h1, h2) and torch.equal(s1, s2)
+    assert (s1.cpu().numpy() == ST_OK).all()
