@@ -131,7 +131,7 @@ bhg_ctx *bhg_create(int device, int flags) {
         return nullptr;
     }
     {
-        std::vector<uint32_t> z(bhg::kZTabWords);
+        std::vector<uint32_t> z(bhg::kZTabAllWords);
         bhg::build_tile_ztab(z.data());
         if (hipMalloc(reinterpret_cast<void **>(&c->ztab), z.size() * 4) != hipSuccess ||
             hipMemcpy(c->ztab, z.data(), z.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -267,7 +267,10 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) kChunkBytes = strtoull(e, nullptr, 10);  // tests
     if (kChunkBytes < 4096) kChunkBytes = 4096;
     const uint32_t max_chunk_n = 1u << 17;
-    const size_t need = al(kChunkBytes + 64) + al((size_t)max_chunk_n * sizeof(bhg_handle)) +
+    // kHead bytes of headroom before each chunk's src bytes: k_decode_tile2 loads a record's head window
+    // from up to 147 B before the record (padding it masks), which must be mapped memory
+    constexpr size_t kHead = 256;
+    const size_t need = kHead + al(kChunkBytes + 64) + al((size_t)max_chunk_n * sizeof(bhg_handle)) +
                         al((size_t)max_chunk_n * sizeof(bhg_desc)) + al((size_t)max_chunk_n * 4);
     for (int k = 0; k < bhg_ctx::kPipe; k++) {
         if (!c->pstream[k]) HIP_TRY(c, hipStreamCreateWithFlags(&c->pstream[k], hipStreamNonBlocking));
@@ -300,7 +303,7 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
             for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
             return -100;  // caller falls back to the whole-batch path
         }
-        uint8_t *base = reinterpret_cast<uint8_t *>(c->pbuf[slot]);
+        uint8_t *base = reinterpret_cast<uint8_t *>(c->pbuf[slot]) + kHead;
         bhg_handle *dh = reinterpret_cast<bhg_handle *>(base + al(kChunkBytes + 64));
         bhg_desc *dd = reinterpret_cast<bhg_desc *>(reinterpret_cast<uint8_t *>(dh) + al((size_t)max_chunk_n * sizeof(bhg_handle)));
         uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(dd) +
@@ -308,7 +311,8 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
                                     : nullptr;
         hipStream_t s = c->pstream[slot];
         // the chunk's handles keep their src-relative offsets: the kernel sees src' = base - lo, src_len' = hi,
-        // and never addresses below base (every in-bounds handle of the chunk has offset >= lo)
+        // and never addresses more than kHead bytes below base (every in-bounds handle of the chunk has
+        // offset >= lo; head windows reach back at most W + 3 bytes)
         if (span) HIP_TRY(c, hipMemcpyAsync(base, src + lo, span, hipMemcpyHostToDevice, s));
         HIP_TRY(c, hipMemcpyAsync(dh, handles + a, (size_t)cn * sizeof(bhg_handle), hipMemcpyHostToDevice, s));
         if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc + a, (size_t)cn * 4, hipMemcpyHostToDevice, s));

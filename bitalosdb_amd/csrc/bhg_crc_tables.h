@@ -158,10 +158,14 @@ inline void crc32c_braid_table(uint64_t fold, uint32_t *out) {
 // Shift tables of the tile decode kernel (bhg_decode_tile.hip), in this order:
 // Z_1024 (Horner step over 8 windows), Z_128, Z_256, Z_512 (window distance
 // to the record end), Z_32 (fold of the 4 interleaved 32-B chains).
-constexpr uint32_t kZTabWords = 5 * 1024;
+// Then the set of k_decode_tile2 (window W = 144 B, two 72-B chains):
+// Z_1152 (Horner over 8 windows), Z_144, Z_288, Z_576, Z_72.
+constexpr uint32_t kZTabWords = 5 * 1024;        // one kernel's set (copied into LDS)
+constexpr uint32_t kZTabAllWords = 2 * kZTabWords;  // both sets, device copy owned by the context
+constexpr uint32_t kTile2Win = 144;
 inline void build_tile_ztab(uint32_t *out) {
-    const uint64_t zs[5] = {1024, 128, 256, 512, 32};
-    for (uint32_t k = 0; k < 5; k++) crc32c_shift_table(zs[k], out + 1024 * k);
+    const uint64_t zs[10] = {1024, 128, 256, 512, 32, 8 * kTile2Win, kTile2Win, 2 * kTile2Win, 4 * kTile2Win, kTile2Win / 2};
+    for (uint32_t k = 0; k < 10; k++) crc32c_shift_table(zs[k], out + 1024 * k);
 }
 
 }  // namespace bhg

@@ -1136,6 +1136,8 @@ hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_
     int variant = L.variant;
     if (codec == BHG_CODEC_NONE && variant == kTileVariant)
         return launch_decode_tile(L, src, src_len, h, n, expected_crc, out);
+    if (codec == BHG_CODEC_NONE && variant == kTile2Variant)
+        return launch_decode_tile2(L, src, src_len, h, n, expected_crc, out);
     if (variant < 0 || variant >= kNumLaneVariants) variant = 28;
     if (codec == BHG_CODEC_NONE)
         launch_lane_mode<MODE_NONE>(L, variant, src, src_len, h, n, expected_crc, out, sizes);

@@ -33,6 +33,10 @@ hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_
 constexpr int kTileVariant = 44;
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out);
+// k_decode_tile2 (variant kTile2Variant): no lane-per-record phase, W = 144 B windows
+constexpr int kTile2Variant = 45;
+hipError_t launch_decode_tile2(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                               const uint32_t *expected_crc, bhg_desc *out);
 hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

@@ -21,12 +21,23 @@ pytestmark = pytest.mark.gpu
 FIELDS = ["key_off", "key_len", "val_off", "val_len", "trailer", "file_num", "fnv1", "crc", "status"]
 
 
-@pytest.fixture(scope="module")
-def codec():
+@pytest.fixture(scope="module", params=["44", "45"], ids=["tile", "tile2"])
+def codec(request):
+    """Every test runs once per NoCompressor tile kernel (k_decode_tile,
+    k_decode_tile2); the variant is read when the context is created."""
+    import os
     from bitalosdb_amd import _lib
     from bitalosdb_amd.codec import BithashCodec
     _lib.lib()
-    c = BithashCodec(0)
+    old = os.environ.get("BHG_DECODE_VARIANT")
+    os.environ["BHG_DECODE_VARIANT"] = request.param
+    try:
+        c = BithashCodec(0)
+    finally:
+        if old is None:
+            os.environ.pop("BHG_DECODE_VARIANT")
+        else:
+            os.environ["BHG_DECODE_VARIANT"] = old
     yield c
     c.close()
 
@@ -274,7 +285,7 @@ def _full_size(codec, synth, handles_tensor, n):
     assert (got["trailer"] >> 8 == np.arange(1, n + 1)).all()
 
 
-@pytest.mark.parametrize("variant", [v for v in range(45) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
+@pytest.mark.parametrize("variant", [v for v in range(46) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
 def test_lane_kernel_variants(variant, monkeypatch):
     """Every CRC-table flavour of k_decode_lane is bit-exact (slice-by-1/4, R=4..32)."""
     from bitalosdb_amd.codec import BithashCodec
@@ -288,6 +299,33 @@ def test_lane_kernel_variants(variant, monkeypatch):
     exp, _, _ = O.decode_batch(src, h)
     assert_desc_equal(got, exp)
     c.close()
+
+
+def test_tile_window_edges(codec):
+    """Record lengths around the 144-B / 128-B window grid of the tile kernels:
+    heads of 1..4 bytes, exactly 8 / 9 / 17 windows, records of 1..3 bytes
+    (raw handles, RECORD_NIL but CRC still reported), arbitrary alignment."""
+    rng = random.Random(77)
+    specs = []
+    for L in list(range(13, 40)) + [140, 143, 144, 145, 146, 147, 148, 149, 287, 288, 289, 290, 291,
+                                    1076, 1151, 1152, 1153, 1154, 1155, 1156, 1157, 1280, 1281, 1296,
+                                    1297, 1300, 2448, 2449, 2453, 4100, 9000]:
+        for kl in (0, 7, 32):
+            vl = L - 12 - 8 - kl
+            if vl >= 1:
+                specs.append((rand_bytes(rng, kl), rand_bytes(rng, vl), rng.randrange(1, 9)))
+    rng.shuffle(specs)
+    src, h = make_records(rng, specs, gap_max=3)
+    extra = [(rng.randrange(0, len(src) - 8), rng.randrange(1, 4), 0) for _ in range(40)]
+    extra += [(rng.randrange(0, len(src) - 300), rng.randrange(4, 300), 0) for _ in range(200)]
+    extra += [(0, 1, 0), (0, 3, 0), (len(src) - 1, 1, 0), (len(src) - 3, 3, 0), (len(src) - 4, 4, 0)]
+    hs = np.concatenate([h, np.array(extra, dtype=O.HANDLE_DT)])
+    order = np.array(list(range(len(hs))))
+    rng.shuffle(order)
+    hs = hs[order]
+    got, _, _ = codec.decode(src, hs)
+    exp, _, _ = O.decode_batch(src, hs)
+    assert_desc_equal(got, exp)
 
 
 @pytest.mark.parametrize("sv", [0, 1])
