@@ -121,7 +121,7 @@ bhg_ctx *bhg_create(int device, int flags) {
     c->variant = bhg::kTileVariant;  // k_decode_tile (bhg_decode_tile.hip); snappy header pass: lane variant 28
     if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
     if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
-    c->snappy_variant = 0;
+    c->snappy_variant = 2;  // k_snappy_rt (bhg_snappy_dec.hip)
     if (const char *s = getenv("BHG_SNAPPY_VARIANT")) c->snappy_variant = atoi(s);
     c->err[0] = 0;
     // blocking stream: orders against the legacy NULL stream, so callers that

@@ -1148,6 +1148,8 @@ hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_
 
 hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
+    if (L.snappy_variant == 2) return launch_snappy_rt(L, src, src_len, h, n, out, out_vals, out_cap, val_off);
+    if (L.snappy_variant == 3) return launch_snappy_grp(L, src, src_len, h, n, out, out_vals, out_cap, val_off);
     if (L.snappy_variant == 0) {
         uint32_t grid = (n + 255) / 256;
         const uint32_t cap = (uint32_t)L.num_cus * 8;

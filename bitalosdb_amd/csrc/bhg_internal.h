@@ -13,7 +13,7 @@ struct Launch {
     int num_cus;        // 256 on MI355X
     int lane_wgs_per_cu;  // override of resident workgroups per CU (0 = variant default)
     int variant;          // lane-kernel variant (bhg_decode.hip kLaneVariants)
-    int snappy_variant;   // 0: lane-per-block snappy decode, 1: wave-per-block
+    int snappy_variant;   // 0: lane-per-block snappy decode, 1: wave-per-block, 2: lane, one round trip per element
     const uint32_t *ztab; // device copy of build_tile_ztab() (owned by the context)
 };
 
@@ -39,6 +39,12 @@ hipError_t launch_decode_tile2(const Launch &L, const uint8_t *src, uint64_t src
                                const uint32_t *expected_crc, bhg_desc *out);
 hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
+// bhg_snappy_dec.hip: lane-per-block snappy decode, one memory round trip per element (snappy_variant 2)
+hipError_t launch_snappy_rt(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
+// bhg_snappy_dec.hip: group-of-8-lanes snappy decode staged in LDS (snappy_variant 3)
+hipError_t launch_snappy_grp(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                             bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

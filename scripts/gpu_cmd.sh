@@ -1,7 +1,7 @@
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/t4
-for d in 0 1 2 3 0; do
-  echo "tile diag $d" >> gpurun_out/t4/lab.txt
-  BHG_TILE_DIAG=$d timeout -k 10 120 scripts/lab/decode_lab 30 =none >> gpurun_out/t4/lab.txt 2>&1 || exit $?
+O=gpurun_out/t8
+mkdir -p $O
+for w in 1 2 4 8; do
+BHG_LANE_WGS_PER_CU=$w BHG_SNAPPY_VARIANT=2 timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 2 --no-cpu > $O/c3_$w.log 2>&1 || exit $?
+echo "wgs/cu $w"; grep '^{' $O/c3_$w.log | cut -c150-330
 done
-cat gpurun_out/t4/lab.txt
