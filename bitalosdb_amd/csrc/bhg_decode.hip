@@ -1150,6 +1150,7 @@ hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
     if (L.snappy_variant == 2) return launch_snappy_rt(L, src, src_len, h, n, out, out_vals, out_cap, val_off);
     if (L.snappy_variant == 3) return launch_snappy_grp(L, src, src_len, h, n, out, out_vals, out_cap, val_off);
+    if (L.snappy_variant == 4) return launch_snappy_rt(L, src, src_len, h, n, out, out_vals, out_cap, val_off, true);
     if (L.snappy_variant == 0) {
         uint32_t grid = (n + 255) / 256;
         const uint32_t cap = (uint32_t)L.num_cus * 8;

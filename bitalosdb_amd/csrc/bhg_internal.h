@@ -41,7 +41,8 @@ hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_
                               bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 // bhg_snappy_dec.hip: lane-per-block snappy decode, one memory round trip per element (snappy_variant 2)
 hipError_t launch_snappy_rt(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
+                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
+                            bool win = false);  // win: tag stream through a per-lane LDS window (snappy_variant 4)
 // bhg_snappy_dec.hip: group-of-8-lanes snappy decode staged in LDS (snappy_variant 3)
 hipError_t launch_snappy_grp(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);

@@ -33,8 +33,13 @@
 // reads per launch for ~1.3 GB of stream + copy-source bytes -- every lane
 // walks its own lines 8-16 B at a time and the lines are evicted between
 // its consecutive touches (profiles/r1_s4_pmc_snappy_rt.json).  Residency
-// 4..32 waves per CU changes the time by < 15 %.  This is the default
-// (snappy_variant 2) and the next kernel to rework.
+// 4..32 waves per CU changes the time by < 15 %.  Knock-outs (timing only):
+// no copy-source loads 2.20 ms / 6.6 GB, no stores 1.95 ms / 12.2 GB, neither
+// 1.24 ms / 6.6 GB -- the tag and literal loads alone fetch 6.6 GB.  Reading
+// the tag stream through a per-lane 128-B LDS window (WIN, snappy_variant 4)
+// cuts the fetch to 8.2 GB but not the time (2.83 ms): the walk is bound by
+// the latency of its dependent element steps, not by HBM bandwidth.  This is
+// the default (snappy_variant 2) and the next kernel to rework.
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -74,11 +79,31 @@ __device__ __forceinline__ void st16_clip(uint64_t a, u32x4 v, uint64_t oe) {
 
 // cp/dst absolute; the stream is [cp, cp + slen), the block's output [dst, dst + dlen);
 // end bounds input reads, oend bounds output reads (the out_vals allocation)
+// WIN: the tag stream is read through a per-lane 128-B LDS window (win, 16-B
+// aligned, 144 B) refilled with 8 whole 16-B loads; without it every tag is an
+// 8-B global load, and at C3 those loads alone fetched 6.6 GB from HBM for
+// 0.58 GB of stream (lines evicted between a lane's consecutive touches)
+template <bool WIN>
 __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uint64_t dst, uint32_t dlen, uint64_t end,
-                                                 uint64_t oend) {
+                                                 uint64_t oend, uint8_t *win = nullptr) {
     const uint64_t oe = dst + dlen;
     uint32_t s = 0, d = 0;
-    uint64_t t8 = slen ? ld64_bounded(cp, end) : 0;
+    uint64_t wb = 0;  // absolute address of win[0]
+    auto tag8 = [&](uint64_t p) -> uint64_t {
+        if (!WIN) return ld64_bounded(p, end);
+        if (wb == 0 || p < wb || p + 8 > wb + 128) {
+            wb = p & ~15ull;
+#pragma unroll
+            for (uint32_t t = 0; t < 8; t++)
+                *reinterpret_cast<u32x4 *>(win + 16 * t) = ld16_hi(wb + 16 * t, end);
+        }
+        const uint32_t q = (uint32_t)(p - wb), qa = q & ~3u, qs = q & 3u;
+        const uint32_t w0 = *reinterpret_cast<const uint32_t *>(win + qa);
+        const uint32_t w1 = *reinterpret_cast<const uint32_t *>(win + qa + 4);
+        const uint32_t w2 = *reinterpret_cast<const uint32_t *>(win + qa + 8);
+        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, qs) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, qs) << 32);
+    };
+    uint64_t t8 = slen ? tag8(cp) : 0;
     while (s < slen) {
         const uint32_t tag = (uint32_t)t8 & 0xffu;
         uint32_t n, R;
@@ -128,7 +153,7 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
             hi = oend;
             lit = false;
         }
-        if (s < slen) t8 = ld64_bounded(cp + s, end);  // next tag: in flight with this element's data
+        if (s < slen) t8 = tag8(cp + s);  // next tag: in flight with this element's data
         const uint64_t o = dst + d;
         for (uint32_t k = 0; k < n;) {
             const uint32_t seg = lit ? (n - k < 64u ? n - k : 64u) : n;  // copies are <= 64 B
@@ -153,10 +178,13 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
     return d == dlen;
 }
 
+template <bool WIN>
 __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off) {
+    __shared__ __attribute__((aligned(16))) uint8_t wins[WIN ? 256 * 144 : 16];
+    uint8_t *win = wins + (WIN ? threadIdx.x * 144 : 0);
     const uint64_t base = (uint64_t)src, end = base + src_len;
     const uint64_t oend = (uint64_t)out_vals + out_cap;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -179,7 +207,7 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
                 hdr++;
                 if (b < 0x80) break;
             }
-            if (!snappy_decode_rt(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end, oend))
+            if (!snappy_decode_rt<WIN>(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end, oend, win))
                 fin = BHG_ST_SNAPPY_CORRUPT;
         }
         dw[2] = 0;
@@ -366,7 +394,7 @@ __global__ __launch_bounds__(64 * WPB) void k_snappy_grp(const uint8_t *__restri
                         hdr++;
                         if (b < 0x80) break;
                     }
-                    r = snappy_decode_rt(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end, oend) ? 1u : 0u;
+                    r = snappy_decode_rt<false>(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end, oend) ? 1u : 0u;
                 }
                 ok = __shfl(r, g * G, 64) != 0;
             }
@@ -383,13 +411,17 @@ __global__ __launch_bounds__(64 * WPB) void k_snappy_grp(const uint8_t *__restri
 }  // namespace
 
 hipError_t launch_snappy_rt(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
+                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off, bool win) {
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * (L.lane_wgs_per_cu > 0 ? L.lane_wgs_per_cu : 8);
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(k_snappy_rt, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals, out_cap,
-                       val_off);
+    if (win)
+        hipLaunchKernelGGL(k_snappy_rt<true>, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
+                           out_cap, val_off);
+    else
+        hipLaunchKernelGGL(k_snappy_rt<false>, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
+                           out_cap, val_off);
     return hipGetLastError();
 }
 

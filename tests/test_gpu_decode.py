@@ -328,7 +328,7 @@ def test_tile_window_edges(codec):
     assert_desc_equal(got, exp)
 
 
-@pytest.mark.parametrize("sv", [0, 1, 2, 3])
+@pytest.mark.parametrize("sv", [0, 1, 2, 3, 4])
 def test_snappy_kernel_variants(sv, monkeypatch):
     """lane-per-block and wave-per-block snappy decoders are both bit-exact."""
     from bitalosdb_amd.codec import BithashCodec
