@@ -113,6 +113,40 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
                 for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
             }
         }
+        // ---------------- phase 2 state; round 0's windows are requested here, before phase 1's
+        // CRC / FNV-1 work, so that work overlaps their memory latency
+        uint32_t mycrc = 0;
+        uint32_t fw[2][33];
+        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
+            const uint32_t sl = 8 * s + rr;
+            const uint32_t Lr = __shfl(L, sl, 64);
+            const uint64_t pr = shfl_u64(p, sl);
+            mm = __shfl(m, sl, 64);
+            wb = pr + (Lr - 128 * (mm - 1));  // start of window 1
+            q0 = (int32_t)(mm - 1) - (int32_t)j;
+            hasw = Lr != 0 && q0 >= 1;
+            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+        };
+        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
+            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
+            if (a + 132 <= end) {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+                }
+                w[32] = gld<uint32_t>(a + 128);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+            }
+        };
+        uint64_t wb;
+        uint32_t mm;
+        int32_t qf, q0;
+        bool hasw;
+        rinfo(0, wb, mm, qf, q0, hasw);
+        if (hasw) load_win(fw[0], wb, qf);
         uint32_t hcrc = 0xffffffffu;  // crc.New: Go's crc32.Update starts from ^0
         uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
         uint64_t trailer = 255;       // InternalKeyKindInvalid when ikeySize < 8
@@ -168,38 +202,6 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             }
         }
         // ---------------- phase 2: 8 rounds; lane (rr, j) on record 8s + rr
-        uint32_t mycrc = 0;
-        uint32_t fw[2][33];
-        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
-            const uint32_t sl = 8 * s + rr;
-            const uint32_t Lr = __shfl(L, sl, 64);
-            const uint64_t pr = shfl_u64(p, sl);
-            mm = __shfl(m, sl, 64);
-            wb = pr + (Lr - 128 * (mm - 1));  // start of window 1
-            q0 = (int32_t)(mm - 1) - (int32_t)j;
-            hasw = Lr != 0 && q0 >= 1;
-            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
-        };
-        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
-            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
-            if (a + 132 <= end) {
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
-                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
-                }
-                w[32] = gld<uint32_t>(a + 128);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
-            }
-        };
-        uint64_t wb;
-        uint32_t mm;
-        int32_t qf, q0;
-        bool hasw;
-        rinfo(0, wb, mm, qf, q0, hasw);
-        if (hasw) load_win(fw[0], wb, qf);
 #pragma unroll
         for (uint32_t s = 0; s < 8; s++) {
             const uint32_t cb = s & 1;
