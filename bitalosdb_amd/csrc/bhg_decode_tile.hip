@@ -63,7 +63,9 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     const uint64_t base = (uint64_t)src, end = base + src_len;
     const uint32_t ntiles = (n + 63) / 64;
     const uint32_t tstride = gridDim.x * WPB;
-    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
+    // wave-major tile index: the waves that take one tile more than the others
+    // (ntiles mod tstride of them) are spread over every CU, not packed on the first ones
+    uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     bhg_handle hn = {0, 0, 0};
     if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
     for (; tile < ntiles; tile += tstride) {
