@@ -31,7 +31,7 @@ EXPORTS = [
     "bhg_abi_version", "bhg_device_count", "bhg_create", "bhg_destroy", "bhg_last_error", "bhg_stream",
     "bhg_stream_sync", "bhg_malloc_device", "bhg_free_device", "bhg_malloc_host", "bhg_free_host",
     "bhg_memcpy_h2d", "bhg_memcpy_d2h", "bhg_memset_device", "bhg_decode_batch", "bhg_decode_batch_host",
-    "bhg_crc32c_masked_batch", "bhg_fnv32_batch", "bhg_encode_batch", "bhg_scan_tables",
+    "bhg_crc32c_masked_batch", "bhg_crc32c_masked_long", "bhg_fnv32_batch", "bhg_encode_batch", "bhg_scan_tables",
     "bhg_host_register", "bhg_host_unregister", "bhg_get_batch",
 ]
 
@@ -81,6 +81,7 @@ def lib():
             "bhg_decode_batch": (I, [P, P, U64, P, U32, I, P, P, P, U64, P, P]),
             "bhg_decode_batch_host": (I, [P, P, U64, P, U32, I, P, P, P, U64, P]),
             "bhg_crc32c_masked_batch": (I, [P, P, U64, P, U32, P, P]),
+            "bhg_crc32c_masked_long": (I, [P, P, U64, P, U32, P, P]),
             "bhg_fnv32_batch": (I, [P, P, U64, P, U32, P, P]),
             "bhg_encode_batch": (I, [P, P, P, P, P, P, U32, I, P, U32, U32, U64, P, U64,
                                      ctypes.POINTER(EncodeOut), P]),

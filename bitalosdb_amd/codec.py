@@ -269,6 +269,16 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_crc32c_masked_batch")
         return out
 
+    def crc_long(self, src_t, handles_t, n):
+        """bhg_crc32c_masked_long: crc.New(range).Value() per range, one workgroup
+        per range (long ranges, e.g. each table's indexhash_data)."""
+        with torch.cuda.stream(self.stream):
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
+        rc = self.L.bhg_crc32c_masked_long(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(out),
+                                           self._stream())
+        B.check(self.ctx, rc, "bhg_crc32c_masked_long")
+        return out
+
     def fnv_batch(self, src_t, handles_t, n):
         with torch.cuda.stream(self.stream):
             out = torch.empty(n, dtype=torch.int32, device=self.device)

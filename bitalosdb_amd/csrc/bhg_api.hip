@@ -422,6 +422,16 @@ int bhg_crc32c_masked_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, co
     return BHG_OK;
 }
 
+int bhg_crc32c_masked_long(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                           uint32_t *out_crc, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (n == 0) return BHG_OK;
+    if (!handles || !out_crc || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    HIP_TRY(c, bhg::launch_crc_long(launch_of(c, stream), src, src_len, handles, n, out_crc));
+    return BHG_OK;
+}
+
 int bhg_fnv32_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
                     uint32_t *out_fnv, void *stream) {
     if (!c) return BHG_EINVAL;

@@ -48,6 +48,9 @@ hipError_t launch_snappy_grp(const Launch &L, const uint8_t *src, uint64_t src_l
                              bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
+// one workgroup per range (long ranges: the per-table indexhash checksum)
+hipError_t launch_crc_long(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                           uint32_t *out);
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 

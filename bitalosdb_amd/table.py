@@ -21,7 +21,7 @@ import struct
 
 import numpy as np
 
-from ._lib import TABLE_DT
+from ._lib import HANDLE_DT, TABLE_DT
 
 RECORD_HEADER_SIZE = 12
 BLOCK_RESTART_INTERVAL = 16          # block.go:607
@@ -158,6 +158,30 @@ def open_table(buf, base=0):
     info = dict(data_bh=meta[META_DATA_BH], conflict_bh=(coff, clen), index_bh=(ioff, ilen),
                 index_data=(index_off, index_len), index_checksum=checksum, meta_bh=(moff, mlen))
     return rec, info
+
+
+def verify_index_checksums(codec, src_t, infos, bases):
+    """The CRC-verify build contract for tables: for each
+    opened table, masked CRC-32C of its indexhash_data on the GPU against the
+    decimal indexhash_checksum that Writer.writeIndexHash stored
+    (bithash/writer.go:476-478).  The reference reader never checks it
+    (reader.go:162-183 reads only indexhash_data).
+
+    codec: BithashCodec; src_t: device bytes holding the tables; infos: the
+    info dicts of open_table; bases: each table's offset in src_t.
+    Returns (ok bool[n], computed uint32[n]); a table without the checksum
+    entry compares as not ok."""
+    from .codec import handles_tensor
+    n = len(infos)
+    h = np.zeros(n, dtype=HANDLE_DT)
+    for t, (info, b) in enumerate(zip(infos, bases)):
+        off, ln = info["index_data"]
+        h[t] = (b + off, ln, 0)
+    if n == 0:
+        return np.zeros(0, dtype=bool), np.zeros(0, dtype=np.uint32)
+    got = codec.crc_long(src_t, handles_tensor(h, codec.device), n).cpu().numpy().view(np.uint32)
+    want = np.array([-1 if i["index_checksum"] is None else i["index_checksum"] for i in infos], dtype=np.int64)
+    return got.astype(np.int64) == want, got
 
 
 # ------------------------------------------------------------------ close (Writer.writeTable)
