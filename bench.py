@@ -36,7 +36,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # GPU clocks ramp over the first ~100 C2 launches (~30 ms of load; profiles/r1_s6_clock_ramp_probe.txt)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--blocks", type=int, default=1_000_000, help="blocks per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")

@@ -32,7 +32,7 @@ for s in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
       cat $OUT/smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $OUT/bench.log 2>&1 || exit $?
+      timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || exit $?
       cat $OUT/bench.log ;;
     benchq)
       timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu --no-e2e > $OUT/benchq.log 2>&1 || exit $?
@@ -40,7 +40,7 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv \
-        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu --no-e2e > $OUT/prof.log 2>&1 || exit $?
+        -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-e2e > $OUT/prof.log 2>&1 || exit $?
       find $OUT/prof -name "*stats*" | head ;;
     c3)
       timeout -k 10 600 python bench.py --config c3 --steps 10 --warmup 2 --cpu-seconds 8 > $OUT/bench_c3.log 2>&1 || exit $?
