@@ -117,6 +117,13 @@ int main(int argc, char **argv) {
     bhg_ctx *ctx = bhg_create(0, 0);
     if (!ctx) { fprintf(stderr, "bhg_create failed\n"); return 1; }
     hipStream_t s = (hipStream_t)bhg_stream(ctx);
+    // clocks ramp over the first ~100 launches (profiles/r1_s6_clock_ramp_probe.txt): warm up first
+    {
+        const int warm = getenv("LAB_WARM") ? atoi(getenv("LAB_WARM")) : 300;
+        for (int it = 0; it < warm; it++)
+            if (bhg_decode_batch(ctx, src, len, dh, n, 0, nullptr, ref, nullptr, 0, nullptr, s) != 0) return 1;
+        CK(hipStreamSynchronize(s));
+    }
     // production reference
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
