@@ -23,7 +23,9 @@ assert HANDLE_DT.itemsize == 16 and DESC_DT.itemsize == 40
 BHG_OK, BHG_EINVAL, BHG_EHIP, BHG_ENOMEM, BHG_ENODEV, BHG_ECAPACITY = 0, -1, -2, -3, -4, -5
 CODEC_NONE, CODEC_SNAPPY = 0, 1
 ST_OK, ST_RECORD_NIL, ST_ILLEGAL_LENGTH, ST_INCOMPLETE, ST_SNAPPY_CORRUPT, ST_SNAPPY_TOO_LARGE, \
-    ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED, ST_NOT_FOUND = range(11)
+    ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED, ST_NOT_FOUND, \
+    ST_NO_SPACE, ST_SKIPPED = range(13)
+ABI_VERSION = 2
 TABLE_DT = np.dtype([("base", "<u8"), ("index_off", "<u8"), ("index_len", "<u8"), ("conflict_off", "<u8"),
                      ("conflict_bh_off", "<u4"), ("conflict_bh_len", "<u4")])
 
@@ -31,7 +33,8 @@ EXPORTS = [
     "bhg_abi_version", "bhg_device_count", "bhg_create", "bhg_destroy", "bhg_last_error", "bhg_stream",
     "bhg_stream_sync", "bhg_malloc_device", "bhg_free_device", "bhg_malloc_host", "bhg_free_host",
     "bhg_memcpy_h2d", "bhg_memcpy_d2h", "bhg_memset_device", "bhg_decode_batch", "bhg_decode_batch_host",
-    "bhg_crc32c_masked_batch", "bhg_crc32c_masked_long", "bhg_fnv32_batch", "bhg_encode_batch", "bhg_scan_tables",
+    "bhg_crc32c_masked_batch", "bhg_crc32c_masked_long", "bhg_fnv32_batch", "bhg_encode_batch",
+    "bhg_encode_ikey_batch", "bhg_scan_tables",
     "bhg_host_register", "bhg_host_unregister", "bhg_get_batch",
 ]
 
@@ -50,10 +53,9 @@ _lib = None
 
 def build(force=False):
     """Compile the HIP sources for gfx950 into lib/libbithashgpu.so (hipcc cross-compiles; no GPU needed)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-j8", "-C", CSRC])
-    else:
-        subprocess.check_call(["make", "-s", "-j8", "-C", CSRC])
+    if force:
+        subprocess.check_call(["make", "-s", "-C", CSRC, "clean"])
+    subprocess.check_call(["make", "-s", "-j8", "-C", CSRC])
 
 
 def lib():
@@ -62,6 +64,8 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise BhgError("libbithashgpu.so not built: run bitalosdb_amd._lib.build() / __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
+        if L.bhg_abi_version() != ABI_VERSION:
+            raise BhgError("libbithashgpu.so ABI %d, bindings expect %d: rebuild" % (L.bhg_abi_version(), ABI_VERSION))
         P, U32, U64, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
         sig = {
             "bhg_abi_version": (I, []),
@@ -83,8 +87,10 @@ def lib():
             "bhg_crc32c_masked_batch": (I, [P, P, U64, P, U32, P, P]),
             "bhg_crc32c_masked_long": (I, [P, P, U64, P, U32, P, P]),
             "bhg_fnv32_batch": (I, [P, P, U64, P, U32, P, P]),
-            "bhg_encode_batch": (I, [P, P, P, P, P, P, U32, I, P, U32, U32, U64, P, U64,
+            "bhg_encode_batch": (I, [P, P, P, P, P, P, U64, U32, I, P, U32, U32, U64, P, U64,
                                      ctypes.POINTER(EncodeOut), P]),
+            "bhg_encode_ikey_batch": (I, [P, P, P, P, P, P, U32, P, P, P, U32, P, U64,
+                                          ctypes.POINTER(EncodeOut), P]),
             "bhg_scan_tables": (I, [P, P, P, U32, I, P, U64, P, P, P]),
             "bhg_host_register": (I, [P, P, U64]),
             "bhg_host_unregister": (I, [P, P]),

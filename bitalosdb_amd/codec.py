@@ -36,6 +36,8 @@ STATUS_ERRORS = {
     B.ST_KEY_TOO_LARGE: "bithash: key too large",                # ErrBhKeyTooLarge
     B.ST_VALUE_TOO_LARGE: "bithash: value too large",            # ErrBhValueTooLarge
     B.ST_DATA_MAX_EXCEEDED: "bithash: panic add exceed data max size",
+    B.ST_NOT_FOUND: "bithash: not found",                        # ErrBhNotFound
+    B.ST_NO_SPACE: "bithash: encode output buffer too small",
 }
 
 
@@ -165,7 +167,9 @@ class BithashCodec:
         return res.desc_np(), None, None
 
     def decode_host(self, src, handles, compressor=NoCompressor, expected_crc=None, out_vals_cap=None):
-        """End-to-end path: host buffers in and out (bhg_decode_batch_host)."""
+        """End-to-end path: host buffers in and out (bhg_decode_batch_host).
+        Snappy with out_vals_cap None runs the sizing pass first (out_vals NULL)
+        and allocates exactly out_val_off[n] bytes."""
         src = np.ascontiguousarray(np.frombuffer(src, np.uint8) if isinstance(src, (bytes, bytearray)) else src,
                                    dtype=np.uint8)
         h = np.ascontiguousarray(handles, dtype=HANDLE_DT)
@@ -176,12 +180,17 @@ class BithashCodec:
         cap = 0
         vals = None
         if compressor == SnappyCompressor:
-            cap = out_vals_cap if out_vals_cap is not None else max(1, int(src.size) * 22)
+            if out_vals_cap is None:
+                rc = self.L.bhg_decode_batch_host(self.ctx, _ptr(src), src.size, _ptr(h), n, compressor, _ptr(exp),
+                                                  _ptr(desc), None, 0, _ptr(off))
+                B.check(self.ctx, rc, "bhg_decode_batch_host(sizing)")
+                out_vals_cap = int(off[-1])
+            cap = out_vals_cap
             vals = np.zeros(max(cap, 1), dtype=np.uint8)
         rc = self.L.bhg_decode_batch_host(self.ctx, _ptr(src), src.size, _ptr(h), n, compressor, _ptr(exp),
                                           _ptr(desc), _ptr(vals), cap, _ptr(off))
         B.check(self.ctx, rc, "bhg_decode_batch_host")
-        return desc, (None if vals is None else vals[:int(off[-1])]), off
+        return desc, (None if vals is None else vals[:min(cap, int(off[-1]))]), off
 
     def get_batch(self, src_t, tables, keys, table_idx, khash=None):
         """Batched Reader.Get index path (bhg_get_batch): returns device tensors
@@ -349,15 +358,41 @@ class EncodeBuffers:
 
 
 def _encode_codec(self, keys_t, key_off_t, trailers_t, vals_t, val_off_t, n, codec, file_nums_t, max_tables,
-                  init_size, table_max, out_t, bufs, stream=None):
-    """Device-resident bhg_encode_batch (all tensors on the codec's device)."""
+                  init_size, table_max, out_t, bufs, stream=None, vals_len=None):
+    """Device-resident bhg_encode_batch (all tensors on the codec's device).
+    vals_len = val_off[n] (defaults to vals_t.numel(), an upper bound)."""
     o = bufs.struct()
+    if vals_len is None:
+        vals_len = vals_t.numel()
     rc = self.L.bhg_encode_batch(self.ctx, _ptr(keys_t), _ptr(key_off_t), _ptr(trailers_t), _ptr(vals_t),
-                                 _ptr(val_off_t), n, codec, _ptr(file_nums_t), max_tables, init_size, table_max,
-                                 _ptr(out_t), out_t.numel(), ctypes.byref(o),
+                                 _ptr(val_off_t), vals_len, n, codec, _ptr(file_nums_t), max_tables, init_size,
+                                 table_max, _ptr(out_t), out_t.numel(), ctypes.byref(o),
                                  stream if stream is not None else self._stream())
     B.check(self.ctx, rc, "bhg_encode_batch")
     return bufs
+
+
+def _encode_ikey_codec(self, keys_t, key_off_t, trailers_t, vals_t, val_off_t, n, khash_t, rec_file_nums_t, live_t,
+                       init_size, out_t, bufs, stream=None):
+    """Device-resident bhg_encode_ikey_batch: BithashWriter.AddIkey over a batch
+    (compaction re-pack, bitree/bithash.go:217-239)."""
+    o = bufs.struct()
+    rc = self.L.bhg_encode_ikey_batch(self.ctx, _ptr(keys_t), _ptr(key_off_t), _ptr(trailers_t), _ptr(vals_t),
+                                      _ptr(val_off_t), n, _ptr(khash_t), _ptr(rec_file_nums_t), _ptr(live_t),
+                                      init_size, _ptr(out_t), out_t.numel(), ctypes.byref(o),
+                                      stream if stream is not None else self._stream())
+    B.check(self.ctx, rc, "bhg_encode_ikey_batch")
+    return bufs
+
+
+def _encode_result(bufs, out, nt):
+    summ = bufs.summary.cpu().numpy().view(np.uint64)
+    total = int(summ[0])
+    u32 = lambda t: t.cpu().numpy().view(np.uint32)
+    return dict(out=out[:min(total, out.numel())].cpu().numpy(), pos=bufs.pos.cpu().numpy().view(np.uint64),
+                bh_off=u32(bufs.bh_off), bh_len=u32(bufs.bh_len), table=u32(bufs.table), fnv=u32(bufs.fnv1),
+                crc=u32(bufs.crc), status=u32(bufs.status), table_start=u32(bufs.table_start)[:nt], ntables=nt,
+                summary=summ.copy())
 
 
 def _encode(self, keys, trailers, values, compressor=NoCompressor, file_nums=(1,), init_size=0,
@@ -377,18 +412,42 @@ def _encode(self, keys, trailers, values, compressor=NoCompressor, file_nums=(1,
         out = torch.zeros(max(out_cap, 1), dtype=torch.uint8, device=dev)
         bufs = EncodeBuffers(n, len(file_nums), dev)
         self.encode_batch(kb, _u64_tensor(key_off, dev), _u64_tensor(trailers, dev), vb, _u64_tensor(val_off, dev),
-                          n, compressor, _u32_tensor(file_nums, dev), len(file_nums), init_size, table_max, out, bufs)
+                          n, compressor, _u32_tensor(file_nums, dev), len(file_nums), init_size, table_max, out, bufs,
+                          vals_len=int(val_off[-1]))
         self.sync()
-        summ = bufs.summary.cpu().numpy().view(np.uint64)
-        nt = int(summ[1])
+        nt = int(bufs.summary.cpu().numpy().view(np.uint64)[1])
         if nt == 0:
             raise ValueError("not enough file numbers for the table splits")
-        total = int(summ[0])
-        u32 = lambda t: t.cpu().numpy().view(np.uint32)
-        return dict(out=out[:total].cpu().numpy(), pos=bufs.pos.cpu().numpy().view(np.uint64), bh_off=u32(bufs.bh_off),
-                    bh_len=u32(bufs.bh_len), table=u32(bufs.table), fnv=u32(bufs.fnv1), crc=u32(bufs.crc),
-                    status=u32(bufs.status), table_start=u32(bufs.table_start)[:nt], ntables=nt)
+        return _encode_result(bufs, out, nt)
+
+
+def _encode_ikey(self, keys, trailers, values, rec_file_nums, live=None, khash=None, init_size=0, out_cap=None):
+    """BithashWriter.AddIkey over a host batch: values are written as given
+    (stored bytes), header fileNum per record, records with live[i] == 0
+    skipped (BHG_ST_SKIPPED).  Results as numpy (oracle-shaped dict)."""
+    dev = self.device
+    with torch.cuda.stream(self.stream):
+        n = len(keys)
+        key_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(k) for k in keys], out=key_off[1:])
+        val_off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(v) for v in values], out=val_off[1:])
+        kb = as_device_bytes(b"".join(keys) or b"\0", dev)
+        vb = as_device_bytes(b"".join(values) or b"\0", dev)
+        if out_cap is None:
+            out_cap = int(sum(20 + len(k) + len(v) for k, v in zip(keys, values))) + 16
+        out = torch.zeros(max(out_cap, 1), dtype=torch.uint8, device=dev)
+        bufs = EncodeBuffers(n, 1, dev)
+        live_t = None if live is None else torch.from_numpy(np.ascontiguousarray(live, dtype=np.uint8)).to(dev)
+        kh_t = None if khash is None else _u32_tensor(khash, dev)
+        self.encode_ikey_batch(kb, _u64_tensor(key_off, dev), _u64_tensor(trailers, dev), vb,
+                               _u64_tensor(val_off, dev), n, kh_t, _u32_tensor(rec_file_nums, dev), live_t, init_size,
+                               out, bufs)
+        self.sync()
+        return _encode_result(bufs, out, 1)
 
 
 BithashCodec.encode_batch = _encode_codec
+BithashCodec.encode_ikey_batch = _encode_ikey_codec
 BithashCodec.encode = _encode
+BithashCodec.encode_ikey = _encode_ikey

@@ -1,7 +1,7 @@
 // bhg_api.hip -- implementation of the C-ABI in include/bithashgpu.h.
 //
-// Host orchestration only: argument checks, per-context scratch, launch
-// sequencing on the caller's stream.  All byte work runs in the kernels
+// Host orchestration only: argument checks, per-call scratch from the
+// context's stream-ordered pool, launch sequencing on the caller's stream.  All byte work runs in the kernels
 // (bhg_decode.hip, bhg_encode.hip, bhg_scan.hip); there is no CPU fallback:
 // without a usable HIP device bhg_create() fails and every entry point
 // returns an error.
@@ -22,17 +22,15 @@ struct bhg_ctx {
     int device;
     hipStream_t stream;
     int num_cus;
-    int lane_wgs_per_cu;
-    int variant;
-    int snappy_variant;
     char err[512];
-    std::mutex mu;          // guards scratch growth and the host-path buffers
-    void *scratch = nullptr;
-    size_t scratch_cap = 0;
+    hipMemPool_t pool = nullptr;  // per-call scratch (stream ordered, never shared between calls)
+    std::mutex mu;                // guards the host-path staging buffers and pipeline streams
     // host (end-to-end) path device buffers
     void *h_src = nullptr; size_t h_src_cap = 0;
     void *h_aux = nullptr; size_t h_aux_cap = 0;
+    void *h_vals = nullptr; size_t h_vals_cap = 0;
     uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
+    uint32_t *stab = nullptr;  // stream-kernel shift tables (bhg_decode_stream.h build_stream_tab)
     // pipelined host path: kPipe slots, each with its own stream and device ring buffers
     static constexpr int kPipe = 3;
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
@@ -65,20 +63,47 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     bhg::Launch L;
     L.stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     L.num_cus = c->num_cus;
-    L.lane_wgs_per_cu = c->lane_wgs_per_cu;
-    L.variant = c->variant;
-    L.snappy_variant = c->snappy_variant;
     L.ztab = c->ztab;
+    L.stab = c->stab;
     return L;
 }
 
-// grow ctx scratch (synchronous; never inside a captured region)
+// Per-call device scratch: carved from one stream-ordered allocation of the
+// context's pool, released on the call's stream when the object goes out of
+// scope -- after every kernel the call enqueued, whatever path returns.
+struct Scratch {
+    hipStream_t s = nullptr;
+    uint8_t *base = nullptr;
+    size_t used = 0, cap = 0;
+    ~Scratch() {
+        if (base) (void)hipFreeAsync(base, s);
+    }
+    static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+    uint8_t *take(size_t bytes) {
+        uint8_t *p = base + used;
+        used += al(bytes);
+        return p;
+    }
+};
+
+int scratch_alloc(bhg_ctx *c, hipStream_t s, size_t bytes, Scratch &sc) {
+    sc.s = s;
+    sc.cap = bytes + 256;
+    void *p = nullptr;
+    hipError_t e = hipMallocFromPoolAsync(&p, sc.cap, c->pool, s);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMallocFromPoolAsync(scratch)");
+    sc.base = reinterpret_cast<uint8_t *>(p);
+    return BHG_OK;
+}
+
+// grow a host-path staging buffer (synchronous; the host paths are synchronous)
 int ensure_buf(bhg_ctx *c, void **buf, size_t *cap, size_t need) {
     if (need <= *cap) return BHG_OK;
     if (*buf) {
-        hipStreamSynchronize(c->stream);
-        hipDeviceSynchronize();
-        hipFree(*buf);
+        (void)hipStreamSynchronize(c->stream);
+        for (int k = 0; k < bhg_ctx::kPipe; k++)
+            if (c->pstream[k]) (void)hipStreamSynchronize(c->pstream[k]);
+        (void)hipFree(*buf);
         *buf = nullptr;
         *cap = 0;
     }
@@ -117,12 +142,6 @@ bhg_ctx *bhg_create(int device, int flags) {
     bhg_ctx *c = new bhg_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    c->lane_wgs_per_cu = 0;
-    c->variant = bhg::kTileVariant;  // k_decode_tile (bhg_decode_tile.hip); snappy header pass: lane variant 28
-    if (const char *s = getenv("BHG_LANE_WGS_PER_CU")) c->lane_wgs_per_cu = atoi(s);
-    if (const char *s = getenv("BHG_DECODE_VARIANT")) c->variant = atoi(s);
-    c->snappy_variant = 2;  // k_snappy_rt (bhg_snappy_dec.hip)
-    if (const char *s = getenv("BHG_SNAPPY_VARIANT")) c->snappy_variant = atoi(s);
     c->err[0] = 0;
     // blocking stream: orders against the legacy NULL stream, so callers that
     // stage buffers on the default stream need no extra event
@@ -130,33 +149,55 @@ bhg_ctx *bhg_create(int device, int flags) {
         delete c;
         return nullptr;
     }
+    bool ok = true;
     {
-        std::vector<uint32_t> z(bhg::kZTabAllWords);
+        hipMemPoolProps pp;
+        memset(&pp, 0, sizeof pp);
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = device;
+        ok = hipMemPoolCreate(&c->pool, &pp) == hipSuccess;
+        // keep freed scratch in the pool: steady-state calls allocate nothing from the driver
+        uint64_t keep = UINT64_MAX;
+        ok = ok && hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess;
+    }
+    if (ok) {
+        std::vector<uint32_t> z(bhg::kZTabWords);
         bhg::build_tile_ztab(z.data());
-        if (hipMalloc(reinterpret_cast<void **>(&c->ztab), z.size() * 4) != hipSuccess ||
-            hipMemcpy(c->ztab, z.data(), z.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            if (c->ztab) hipFree(c->ztab);
-            hipStreamDestroy(c->stream);
-            delete c;
-            return nullptr;
-        }
+        ok = hipMalloc(reinterpret_cast<void **>(&c->ztab), z.size() * 4) == hipSuccess &&
+             hipMemcpy(c->ztab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (ok) {
+        std::vector<uint32_t> z(bhg::stream_tab_words());
+        bhg::build_stream_tab_default(z.data());
+        ok = hipMalloc(reinterpret_cast<void **>(&c->stab), z.size() * 4) == hipSuccess &&
+             hipMemcpy(c->stab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (!ok) {
+        bhg_destroy(c);
+        return nullptr;
     }
     return c;
 }
 
 void bhg_destroy(bhg_ctx *c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
-    if (c->scratch) hipFree(c->scratch);
-    if (c->h_src) hipFree(c->h_src);
-    if (c->h_aux) hipFree(c->h_aux);
-    if (c->ztab) hipFree(c->ztab);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int k = 0; k < bhg_ctx::kPipe; k++) {
-        if (c->pstream[k]) { hipStreamSynchronize(c->pstream[k]); hipStreamDestroy(c->pstream[k]); }
-        if (c->pbuf[k]) hipFree(c->pbuf[k]);
+        if (c->pstream[k]) { (void)hipStreamSynchronize(c->pstream[k]); (void)hipStreamDestroy(c->pstream[k]); }
+        if (c->pbuf[k]) (void)hipFree(c->pbuf[k]);
     }
-    hipStreamDestroy(c->stream);
+    if (c->h_src) (void)hipFree(c->h_src);
+    if (c->h_aux) (void)hipFree(c->h_aux);
+    if (c->h_vals) (void)hipFree(c->h_vals);
+    if (c->ztab) (void)hipFree(c->ztab);
+    if (c->stab) (void)hipFree(c->stab);
+    if (c->pool) {
+        (void)hipDeviceSynchronize();  // frees enqueued on caller streams have completed
+        (void)hipMemPoolDestroy(c->pool);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -237,15 +278,13 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
-    HIP_TRY(c, bhg::launch_decode_lane(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
+    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
     if (codec == BHG_CODEC_SNAPPY) {
-        {
-            std::lock_guard<std::mutex> g(c->mu);
-            if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(n))) return r;
-        }
-        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, c->scratch));
-        HIP_TRY(c, bhg::launch_snappy_wave(L, src, src_len, handles, n, out_desc, out_vals, out_vals ? out_vals_cap : 0,
-                                           out_val_off));
+        Scratch sc;
+        if (int r = scratch_alloc(c, L.stream, bhg::scan_scratch_bytes(n), sc)) return r;
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
+        if (out_vals)
+            HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off));
     }
     return BHG_OK;
 }
@@ -267,8 +306,8 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) kChunkBytes = strtoull(e, nullptr, 10);  // tests
     if (kChunkBytes < 4096) kChunkBytes = 4096;
     const uint32_t max_chunk_n = 1u << 17;
-    // kHead bytes of headroom before each chunk's src bytes: k_decode_tile2 loads a record's head window
-    // from up to 147 B before the record (padding it masks), which must be mapped memory
+    // kHead bytes of headroom before each chunk's src bytes: the decode kernels may load (and mask) a
+    // window that starts up to 131 B before a record, which must be mapped memory
     constexpr size_t kHead = 256;
     const size_t need = kHead + al(kChunkBytes + 64) + al((size_t)max_chunk_n * sizeof(bhg_handle)) +
                         al((size_t)max_chunk_n * sizeof(bhg_desc)) + al((size_t)max_chunk_n * 4);
@@ -318,7 +357,7 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
         if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc + a, (size_t)cn * 4, hipMemcpyHostToDevice, s));
         bhg::Launch Ls = L;
         Ls.stream = s;
-        HIP_TRY(c, bhg::launch_decode_lane(Ls, base - lo, hi, dh, cn, BHG_CODEC_NONE, de, dd, nullptr));
+        HIP_TRY(c, bhg::launch_decode(Ls, base - lo, hi, dh, cn, BHG_CODEC_NONE, de, dd, nullptr));
         HIP_TRY(c, hipMemcpyAsync(out_desc + a, dd, (size_t)cn * sizeof(bhg_desc), hipMemcpyDeviceToHost, s));
         a = b;
         slot = (slot + 1) % bhg_ctx::kPipe;
@@ -333,6 +372,7 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
                           int codec, const uint32_t *expected_crc, bhg_desc *out_desc, uint8_t *out_vals,
                           uint64_t out_vals_cap, uint64_t *out_val_off) {
     if (!c) return BHG_EINVAL;
+    if (codec != BHG_CODEC_NONE && codec != BHG_CODEC_SNAPPY) { set_err(c, "bad codec %d", codec); return BHG_EINVAL; }
     if (n == 0) {
         if (codec == BHG_CODEC_SNAPPY && out_val_off) out_val_off[0] = 0;
         return BHG_OK;
@@ -341,7 +381,7 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     std::lock_guard<std::mutex> g(c->mu);
-    if (codec == BHG_CODEC_NONE && !getenv("BHG_HOST_NOPIPE")) {
+    if (codec == BHG_CODEC_NONE) {
         bool sorted = true;
         for (uint32_t i = 1; i < n && sorted; i++) sorted = handles[i].offset >= handles[i - 1].offset;
         if (sorted) {
@@ -351,32 +391,36 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     }
     const size_t hb = (size_t)n * sizeof(bhg_handle), db = (size_t)n * sizeof(bhg_desc);
     const size_t eb = expected_crc ? (size_t)n * 4 : 0, ob = codec == BHG_CODEC_SNAPPY ? ((size_t)n + 1) * 8 : 0;
-    const size_t vb = codec == BHG_CODEC_SNAPPY ? (size_t)out_vals_cap : 0;
+    const size_t sb = codec == BHG_CODEC_SNAPPY ? bhg::scan_scratch_bytes(n) : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     if (int r = ensure_buf(c, &c->h_src, &c->h_src_cap, src_len + 64)) return r;
-    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(vb) + 256)) return r;
+    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(sb) + 256)) return r;
     uint8_t *a = reinterpret_cast<uint8_t *>(c->h_aux);
     bhg_handle *dh = reinterpret_cast<bhg_handle *>(a); a += al(hb);
     bhg_desc *dd = reinterpret_cast<bhg_desc *>(a); a += al(db);
     uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(eb);
     uint64_t *doff = ob ? reinterpret_cast<uint64_t *>(a) : nullptr; a += al(ob);
-    uint8_t *dv = vb ? a : nullptr;
+    void *dscan = sb ? a : nullptr;
     hipStream_t s = c->stream;
     HIP_TRY(c, hipMemcpyAsync(c->h_src, src, src_len, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(dh, handles, hb, hipMemcpyHostToDevice, s));
     if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc, eb, hipMemcpyHostToDevice, s));
     bhg::Launch L = launch_of(c, nullptr);
-    HIP_TRY(c, bhg::launch_decode_lane(L, reinterpret_cast<const uint8_t *>(c->h_src), src_len, dh, n, codec, de, dd, doff));
+    const uint8_t *dsrc = reinterpret_cast<const uint8_t *>(c->h_src);
+    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, codec, de, dd, doff));
     if (codec == BHG_CODEC_SNAPPY) {
-        if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(n))) return r;
-        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, doff, doff, n, c->scratch));
-        HIP_TRY(c, bhg::launch_snappy_wave(L, reinterpret_cast<const uint8_t *>(c->h_src), src_len, dh, n, dd, dv,
-                                           dv ? out_vals_cap : 0, doff));
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, doff, doff, n, dscan));
         HIP_TRY(c, hipMemcpyAsync(out_val_off, doff, ob, hipMemcpyDeviceToHost, s));
         HIP_TRY(c, hipStreamSynchronize(s));
-        uint64_t total = out_val_off[n];
-        if (total > out_vals_cap) total = out_vals_cap;
-        if (total && out_vals) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
+        if (out_vals) {
+            // the device value buffer is sized from the scanned total, capped by what the caller can take
+            uint64_t total = out_val_off[n];
+            if (total > out_vals_cap) total = out_vals_cap;
+            if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 64)) return r;
+            uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals);
+            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff));
+            if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
+        }
     }
     HIP_TRY(c, hipMemcpyAsync(out_desc, dd, db, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -442,12 +486,34 @@ int bhg_fnv32_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_
     return BHG_OK;
 }
 
+namespace {
+
+bool encode_outputs_ok(bhg_ctx *c, const bhg_encode_out *o, uint32_t n, uint32_t max_tables) {
+    if (!o || !o->table_start || !o->summary || max_tables < 1) { set_err(c, "bad encode outputs"); return false; }
+    if (n && (!o->pos || !o->bh_off || !o->bh_len || !o->table || !o->fnv1 || !o->crc || !o->status)) {
+        set_err(c, "null buffer");
+        return false;
+    }
+    return true;
+}
+
+// empty batch: summary {0, 1, 0, 0}, table_start[0] = 0
+int encode_empty(bhg_ctx *c, const bhg_encode_out *o, hipStream_t s) {
+    static const uint64_t summ[4] = {0, 1, 0, 0};
+    HIP_TRY(c, hipMemcpyAsync(o->summary, summ, 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemsetAsync(o->table_start, 0, 4, s));
+    return BHG_OK;
+}
+
+}  // namespace
+
 int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
-                     const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec, const uint32_t *file_nums,
-                     uint32_t max_tables, uint32_t init_size, uint64_t table_max, uint8_t *out, uint64_t out_cap,
-                     const bhg_encode_out *o, void *stream) {
+                     const uint8_t *vals, const uint64_t *val_off, uint64_t vals_len, uint32_t n, int codec,
+                     const uint32_t *file_nums, uint32_t max_tables, uint32_t init_size, uint64_t table_max,
+                     uint8_t *out, uint64_t out_cap, const bhg_encode_out *o, void *stream) {
     if (!c) return BHG_EINVAL;
-    if (!o || !o->table_start || !o->summary || max_tables < 1 || !file_nums) { set_err(c, "bad encode outputs"); return BHG_EINVAL; }
+    if (!encode_outputs_ok(c, o, n, max_tables)) return BHG_EINVAL;
+    if (!file_nums) { set_err(c, "null file_nums"); return BHG_EINVAL; }
     if (codec != BHG_CODEC_NONE && codec != BHG_CODEC_SNAPPY) { set_err(c, "bad codec %d", codec); return BHG_EINVAL; }
     // DATA_MAX_EXCEEDED (writer.go:266-269) cannot trigger when size < table_max and
     // table_max + max record <= dataMaxSize; larger tables are rejected up front.
@@ -458,44 +524,31 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     }
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
-    if (n == 0) {
-        HIP_TRY(c, hipMemsetAsync(o->summary, 0, 32, L.stream));
-        uint64_t one = 1;
-        HIP_TRY(c, hipMemcpyAsync(o->summary + 1, &one, 8, hipMemcpyHostToDevice, L.stream));
-        HIP_TRY(c, hipMemsetAsync(o->table_start, 0, 4, L.stream));
-        return BHG_OK;
-    }
-    if (!keys || !key_off || !trailers || !vals || !val_off || !out || !o->pos || !o->bh_off || !o->bh_len ||
-        !o->table || !o->fnv1 || !o->crc || !o->status) {
-        set_err(c, "null buffer");
-        return BHG_EINVAL;
-    }
-    std::lock_guard<std::mutex> g(c->mu);
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t lens_b = al(((size_t)n + 1) * 8), vlen_b = al(((size_t)n + 1) * 8), scan_b = al(bhg::scan_scratch_bytes(n));
+    if (n == 0) return encode_empty(c, o, L.stream);
+    if (!keys || !key_off || !trailers || !vals || !val_off || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    const size_t lens_b = ((size_t)n + 1) * 8, vlen_b = ((size_t)n + 1) * 8, scan_b = bhg::scan_scratch_bytes(n);
     size_t snap_b = 0, soff_b = 0, gt_b = 0;
-    uint64_t vbytes = 0;
     if (codec == BHG_CODEC_SNAPPY) {
-        // bound of the compressed scratch: sum MaxEncodedLen <= 32 n + V + V/6 (needs V = val_off[n])
-        HIP_TRY(c, hipMemcpyAsync(&vbytes, val_off + n, 8, hipMemcpyDeviceToHost, L.stream));
-        HIP_TRY(c, hipStreamSynchronize(L.stream));
-        snap_b = al((size_t)(32ull * n + vbytes + vbytes / 6 + 64));
-        soff_b = al(((size_t)n + 1) * 8);
-        gt_b = al((size_t)bhg::snappy_enc_grid(L, n) * 16384 * 2);
+        // sum MaxEncodedLen = 32 n + V + sum(v_i / 6) <= 32 n + V + V / 6 (encode.go MaxEncodedLen)
+        snap_b = (size_t)(32ull * n + vals_len + vals_len / 6 + 64);
+        soff_b = ((size_t)n + 1) * 8;
+        gt_b = (size_t)bhg::snappy_enc_grid(L, n) * 16384 * 2;
     }
-    if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b)) return r;
-    uint8_t *sp = reinterpret_cast<uint8_t *>(c->scratch);
+    Scratch sc;
+    const size_t al5 = 5 * 256;
+    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b + al5, sc)) return r;
     bhg::EncodeLaunch E;
-    E.lens = reinterpret_cast<uint64_t *>(sp);
-    uint64_t *vlen = reinterpret_cast<uint64_t *>(sp + lens_b);
-    E.scan_scratch = sp + lens_b + vlen_b;
+    memset(&E, 0, sizeof E);
+    E.lens = reinterpret_cast<uint64_t *>(sc.take(lens_b));
+    uint64_t *vlen = reinterpret_cast<uint64_t *>(sc.take(vlen_b));
+    E.scan_scratch = sc.take(scan_b);
     if (codec == BHG_CODEC_SNAPPY) {
-        uint8_t *snap = sp + lens_b + vlen_b + scan_b;
-        uint64_t *soff = reinterpret_cast<uint64_t *>(snap + snap_b);
-        uint16_t *gt = reinterpret_cast<uint16_t *>(snap + snap_b + soff_b);
+        uint8_t *snap = sc.take(snap_b);
+        uint64_t *soff = reinterpret_cast<uint64_t *>(sc.take(soff_b));
+        uint16_t *gt = reinterpret_cast<uint16_t *>(sc.take(gt_b));
         HIP_TRY(c, bhg::launch_snappy_maxlen(L, val_off, n, soff));
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, soff, soff, n, E.scan_scratch));
-        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, soff, vlen, gt));
+        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, snap_b, soff, vlen, gt));
         E.vbase = snap; E.vpos = soff; E.vlen = vlen;
     } else {
         HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
@@ -503,6 +556,38 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     }
     E.keys = keys; E.key_off = key_off; E.trailers = trailers;
     E.n = n; E.file_nums = file_nums; E.max_tables = max_tables; E.init_size = init_size; E.table_max = table_max;
+    E.out = out; E.out_cap = out_cap; E.o = *o;
+    HIP_TRY(c, bhg::launch_encode(L, E));
+    return BHG_OK;
+}
+
+int bhg_encode_ikey_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                          const uint8_t *vals, const uint64_t *val_off, uint32_t n, const uint32_t *khash,
+                          const uint32_t *rec_file_nums, const uint8_t *live, uint32_t init_size, uint8_t *out,
+                          uint64_t out_cap, const bhg_encode_out *o, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (!encode_outputs_ok(c, o, n, 1)) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    if (n == 0) return encode_empty(c, o, L.stream);
+    if (!keys || !key_off || !trailers || !vals || !val_off || !out || !rec_file_nums) {
+        set_err(c, "null buffer");
+        return BHG_EINVAL;
+    }
+    const size_t lens_b = ((size_t)n + 1) * 8, vlen_b = ((size_t)n + 1) * 8, scan_b = bhg::scan_scratch_bytes(n);
+    Scratch sc;
+    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + 3 * 256, sc)) return r;
+    bhg::EncodeLaunch E;
+    memset(&E, 0, sizeof E);
+    E.lens = reinterpret_cast<uint64_t *>(sc.take(lens_b));
+    uint64_t *vlen = reinterpret_cast<uint64_t *>(sc.take(vlen_b));
+    E.scan_scratch = sc.take(scan_b);
+    HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
+    E.vbase = vals; E.vpos = val_off; E.vlen = vlen;
+    E.keys = keys; E.key_off = key_off; E.trailers = trailers; E.n = n;
+    E.file_nums = rec_file_nums;  // unused for the header (rec_file_nums wins); table 0's entry is record 0's
+    E.rec_file_nums = rec_file_nums; E.live = live; E.khash = khash; E.single_table = 1;
+    E.max_tables = 1; E.init_size = init_size; E.table_max = UINT64_MAX;
     E.out = out; E.out_cap = out_cap; E.o = *o;
     HIP_TRY(c, bhg::launch_encode(L, E));
     return BHG_OK;
@@ -517,12 +602,9 @@ int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, u
     if (!src || !table_off || (!out_handles && max_out)) { set_err(c, "null buffer"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        if (int r = ensure_buf(c, &c->scratch, &c->scratch_cap, bhg::scan_scratch_bytes(ntables))) return r;
-    }
-    HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end,
-                                 c->scratch));
+    Scratch sc;
+    if (int r = scratch_alloc(c, L.stream, bhg::scan_scratch_bytes(ntables), sc)) return r;
+    HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, sc.base));
     return BHG_OK;
 }
 

@@ -59,6 +59,28 @@ struct Crc4Perm {
         const uint32_t x = c ^ w;
         return look<3, 0>(x) ^ look<2, 1>(x) ^ look<1, 2>(x) ^ look<0, 3>(x);
     }
+    // word() on (w & keep), keep = 0 or ~0 per lane, with the state zeroed with it: one
+    // 3-input bit op instead of the xor (the stream kernel's head-window padding)
+    __device__ __forceinline__ uint32_t word_and(uint32_t c, uint32_t w, uint32_t keep) const {
+        const uint32_t x = (c ^ w) & keep;
+        return look<3, 0>(x) ^ look<2, 1>(x) ^ look<1, 2>(x) ^ look<0, 3>(x);
+    }
+    // absorb the low nb (0..3) bytes of x in ONE round of independent lookups
+    // (slice-by-nb: T_{nb-1-i} for byte i of c ^ x)
+    __device__ __forceinline__ uint32_t absorb_upto3(uint32_t c, uint32_t x, uint32_t nb) const {
+        const uint32_t m = (1u << (8 * nb)) - 1u;  // nb <= 3
+        const uint32_t y = c ^ (x & m);
+        uint32_t r = nb ? (y >> (8 * nb)) : y;
+#pragma unroll
+        for (uint32_t i = 0; i < 3; i++) {
+            const uint32_t k = nb > i ? nb - 1 - i : 0u;
+            const uint32_t lbk = ((k >> 1) << 16) | ((k & 1u) << 7) | (lb[0] & 0x7cu);  // lb[0] & 0x7c = replica
+            const uint32_t a = __builtin_amdgcn_perm(y, lbk, 0x0c020000u | ((4u + i) << 8));
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(base + a);
+            r ^= nb > i ? v : 0u;
+        }
+        return r;
+    }
     __device__ __forceinline__ uint32_t step(uint32_t c) const { return (c >> 8) ^ look<0, 0>(c); }
     // absorb the low nb (0..4) bytes of x
     __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const {
@@ -156,16 +178,13 @@ inline void crc32c_braid_table(uint64_t fold, uint32_t *out) {
 }
 
 // Shift tables of the tile decode kernel (bhg_decode_tile.hip), in this order:
-// Z_1024 (Horner step over 8 windows), Z_128, Z_256, Z_512 (window distance
-// to the record end), Z_32 (fold of the 4 interleaved 32-B chains).
-// Then the set of k_decode_tile2 (window W = 144 B, two 72-B chains):
-// Z_1152 (Horner over 8 windows), Z_144, Z_288, Z_576, Z_72.
-constexpr uint32_t kZTabWords = 5 * 1024;        // one kernel's set (copied into LDS)
-constexpr uint32_t kZTabAllWords = 2 * kZTabWords;  // both sets, device copy owned by the context
-constexpr uint32_t kTile2Win = 144;
+// Z_1024 (Horner step over 8 windows; also k_crc_long's base), Z_128, Z_256,
+// Z_512 (window distance to the record end), Z_32 (fold of the 4 interleaved
+// 32-B chains).  Device copy owned by the context.
+constexpr uint32_t kZTabWords = 5 * 1024;
 inline void build_tile_ztab(uint32_t *out) {
-    const uint64_t zs[10] = {1024, 128, 256, 512, 32, 8 * kTile2Win, kTile2Win, 2 * kTile2Win, 4 * kTile2Win, kTile2Win / 2};
-    for (uint32_t k = 0; k < 10; k++) crc32c_shift_table(zs[k], out + 1024 * k);
+    const uint64_t zs[5] = {1024, 128, 256, 512, 32};
+    for (uint32_t k = 0; k < 5; k++) crc32c_shift_table(zs[k], out + 1024 * k);
 }
 
 }  // namespace bhg

@@ -269,267 +269,6 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_decode_tile2: same outputs as k_decode_tile, with no lane-per-record
-// phase.  A wave takes tiles of 64 consecutive handles and walks them in 8
-// rounds of 8 records; in round s the 8 lanes (rr, j) of group rr own record
-// 8s + rr completely:
-//   * lane j CRCs the record's windows q = j, j+8, ... of W = 144 B, aligned
-//     to the record END (window 0, the head, is virtually left-padded to W
-//     bytes).  The load of round s+1's windows (148 B from a 4-aligned
-//     address, ~9.2 KB contiguous per wave) is issued before round s is
-//     absorbed.  Go's crc32 init (state ^0) is folded in by inverting record
-//     bytes 0..3 and zeroing the padding: leading zeros leave crc_0 at 0 and
-//     crc_{~0}(M) = crc_0(M ^ (ff ff ff ff 00 ..)) for |M| >= 4 (records of
-//     1..3 bytes take a direct path).  Every window runs the same code, so
-//     the head costs no divergence.
-//   * a window is two 72-B chains folded with Z_72; a lane's windows are
-//     Horner-folded with Z_{8W}; lane j's sum is shifted by Z_{W d}
-//     (d = m-1-q_last, three conditional table steps) and the 8 lanes
-//     xor-reduce, leaving the record state on all 8 lanes;
-//   * all 8 lanes parse the header / UserKey / trailer / FNV-1 from the
-//     record's first 64 B (L1-resident: the same lines as the head window),
-//     and lane j < 5 stores 8 B of the 40-B descriptor: one 320-B contiguous
-//     store per round instead of 64 scattered 40-B writes.
-// LDS: Crc4Perm (128 KiB) + five 4-KiB Z tables -> one 512-thread workgroup
-// per CU.  Reference semantics as k_decode_tile.
-//
-// Status: bit-exact (tests/test_gpu_decode.py runs every case on both tile
-// kernels) but SLOWER at C2: 0.389 ms vs 0.285 ms for k_decode_tile.
-// Knock-out timings on MI355X (outputs wrong by construction): no head
-// loads 0.330, no header parse 0.339, no head_fix 0.351, no CRC table
-// steps 0.324, all four off 0.252 -- the 8x-redundant per-group header work
-// and the padding fix cost more than the lane-per-record phase they replace.
-// Kept as variant 45 (BHG_DECODE_VARIANT) for further work.
-// ---------------------------------------------------------------------------
-namespace {
-
-// dword at the 4-aligned address a; bytes outside [lo, hi) read as 0
-__device__ __forceinline__ uint32_t ld32_in(uint64_t a, uint64_t lo, uint64_t hi) {
-    if (a >= lo && a + 4 <= hi) return gld<uint32_t>(a);
-    uint32_t w = 0;
-    for (uint32_t b = 0; b < 4; b++)
-        if (a + b >= lo && a + b < hi) w |= (uint32_t)gld<uint8_t>(a + b) << (8 * b);
-    return w;
-}
-
-// window word t = u - uA positions relative to the word holding record byte 0
-// (m0 keeps the record bytes of that word): padding -> 0, record bytes 0..3
-// inverted (Go's ^0 initial state), everything else unchanged
-__device__ __forceinline__ uint32_t head_fix(uint32_t x, int32_t t, uint32_t m0) {
-    x = t < 0 ? 0u : x;
-    x = t == 0 ? (~x & m0) : x;
-    x = t == 1 ? (x ^ ~m0) : x;
-    return x;
-}
-
-}  // namespace
-
-template <int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_decode_tile2(const uint8_t *__restrict__ src, uint64_t src_len,
-                                                           const bhg_handle *__restrict__ handles, uint32_t n,
-                                                           const uint32_t *__restrict__ expected_crc,
-                                                           bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
-    constexpr uint32_t W = kTile2Win, NW = W / 4, HW = NW / 2;
-    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Perm::kWords];
-    __shared__ __attribute__((aligned(16))) uint32_t Z[kZTabWords];  // Z_8W, Z_W, Z_2W, Z_4W, Z_W/2
-    Crc4Perm::fill(T);
-    for (uint32_t t = threadIdx.x; t < kZTabWords; t += 64 * WPB) Z[t] = gz[kZTabWords + t];
-    __syncthreads();
-    const Crc4Perm crc(T);
-    const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
-    const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint32_t ntiles = (n + 63) / 64;
-    const uint32_t tstride = gridDim.x * WPB;
-    uint32_t tile = blockIdx.x * WPB + (threadIdx.x >> 6);
-    bhg_handle hn = {0, 0, 0};
-    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
-
-    auto load_win = [&](uint32_t *w, uint64_t pr, uint32_t Lr, uint32_t mr, uint32_t q) {
-        const uint64_t a = (pr + Lr - (uint64_t)W * (mr - q)) & ~3ull;  // may start before the record (head)
-        if (a >= base && a + 4 * (NW + 1) <= end) {
-#pragma unroll
-            for (uint32_t t = 0; t < NW / 4; t++) {
-                const u32x4 x = gld<u32x4_a4>(a + 16 * t);
-                w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
-            }
-            w[NW] = gld<uint32_t>(a + 4 * NW);
-        } else {
-#pragma unroll
-            for (uint32_t t = 0; t <= NW; t++) w[t] = ld32_in(a + 4 * t, base, end);
-        }
-    };
-    auto load_head = [&](uint32_t *hw, uint64_t pr, uint32_t Lr) {
-        const uint64_t a = pr & ~3ull;
-        if (Lr != 0 && a + 64 <= end) {
-#pragma unroll
-            for (uint32_t t = 0; t < 4; t++) {
-                const u32x4 x = gld<u32x4_a4>(a + 16 * t);
-                hw[4 * t] = x.x; hw[4 * t + 1] = x.y; hw[4 * t + 2] = x.z; hw[4 * t + 3] = x.w;
-            }
-        } else if (Lr != 0) {
-#pragma unroll
-            for (uint32_t t = 0; t < 16; t++) hw[t] = ld32_safe(a + 4 * t, end);
-        } else {
-#pragma unroll
-            for (uint32_t t = 0; t < 16; t++) hw[t] = 0;
-        }
-    };
-
-    for (; tile < ntiles; tile += tstride) {
-        const bhg_handle h = hn;
-        {
-            const uint32_t tn = tile + tstride;
-            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
-        }
-        // owner lane = record tile*64 + lane: Reader.readData's handle checks
-        uint32_t st = BHG_ST_OK;
-        bool inb = false;
-        if (tile * 64 + lane < n) {
-            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;                      // reader.go:234-236
-            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset)
-                st = BHG_ST_INCOMPLETE;                                         // reader.go:251-258
-            else inb = true;
-        }
-        const uint32_t Lo = inb ? h.length : 0u;
-        const uint64_t po = base + (inb ? h.offset : 0ull);
-
-        uint32_t fw[2][NW + 1], hb[2][16];
-        uint64_t pn = shfl_u64(po, rr);
-        uint32_t Ln = __shfl(Lo, rr, 64), mn = (Ln + W - 1) / W;
-        if (j < mn) load_win(fw[0], pn, Ln, mn, j);
-        load_head(hb[0], pn, Ln);
-        for (uint32_t s2 = 0; s2 < 8; s2 += 2) {
-#pragma unroll
-            for (uint32_t cb = 0; cb < 2; cb++) {
-                const uint32_t s = s2 + cb;
-                const uint64_t pr = pn;
-                const uint32_t Lr = Ln, mr = mn;
-                if (s + 1 < 8) {
-                    const uint32_t sl = 8 * (s + 1) + rr;
-                    pn = shfl_u64(po, sl);
-                    Ln = __shfl(Lo, sl, 64);
-                    mn = (Ln + W - 1) / W;
-                    if (j < mn) load_win(fw[cb ^ 1], pn, Ln, mn, j);
-                    load_head(hb[cb ^ 1], pn, Ln);
-                }
-                // ---- CRC: windows q = j, j+8, ... of record 8s + rr
-                uint32_t acc = 0, d = 0;
-                if (j < mr) {
-                    for (uint32_t q = j;; q += 8) {
-                        const uint64_t vs = pr + Lr - (uint64_t)W * (mr - q);
-                        const uint32_t sh = (uint32_t)(vs & 3);
-                        int64_t o64 = (int64_t)W * (int64_t)(mr - q) - (int64_t)Lr;  // record byte 0, window-relative
-                        const int32_t o = o64 < -8 ? -8 : (int32_t)o64;
-                        const int32_t uA = o >> 2;
-                        const uint32_t m0 = 0xffffffffu << (8 * (uint32_t)(o & 3));
-                        uint32_t c0 = 0, c1 = 0;
-#pragma unroll
-                        for (uint32_t u = 0; u < HW; u++) {
-                            uint32_t x0 = __builtin_amdgcn_alignbyte(fw[cb][u + 1], fw[cb][u], sh);
-                            uint32_t x1 = __builtin_amdgcn_alignbyte(fw[cb][u + HW + 1], fw[cb][u + HW], sh);
-                            x0 = head_fix(x0, (int32_t)u - uA, m0);
-                            x1 = head_fix(x1, (int32_t)(u + HW) - uA, m0);
-                            c0 = crc.word(c0, x0);
-                            c1 = crc.word(c1, x1);
-                        }
-                        uint32_t V = zapply(Z + 4096, c0) ^ c1;
-                        if (q != j) V ^= zapply(Z, acc);
-                        acc = V;
-                        if (q + 8 >= mr) {
-                            d = mr - 1 - q;
-                            break;
-                        }
-                        load_win(fw[cb], pr, Lr, mr, q + 8);  // records longer than 8 windows (synchronous)
-                    }
-                }
-                if (d & 1) acc = zapply(Z + 1024, acc);
-                if (d & 2) acc = zapply(Z + 2048, acc);
-                if (d & 4) acc = zapply(Z + 3072, acc);
-                acc ^= __shfl_xor(acc, 1, 64);
-                acc ^= __shfl_xor(acc, 2, 64);
-                acc ^= __shfl_xor(acc, 4, 64);
-                const uint32_t hsh = (uint32_t)(pr & 3);
-                if (Lr != 0 && Lr < 4)  // the byte-0..3 inversion needs 4 record bytes
-                    acc = crc.partial(0xffffffffu, __builtin_amdgcn_alignbyte(hb[cb][1], hb[cb][0], hsh), Lr);
-                // ---- readRecordHeader / readRecord / readKV on all 8 lanes of the group
-                const uint32_t r = 8 * s + rr, ri = tile * 64 + r;
-                const uint32_t str = __shfl(st, r, 64);
-                uint32_t rw[14];
-#pragma unroll
-                for (int u = 0; u < 14; u++) rw[u] = __builtin_amdgcn_alignbyte(hb[cb][u + 1], hb[cb][u], hsh);
-                uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
-                uint64_t trailer = 255;  // InternalKeyKindInvalid when ikeySize < 8
-                bool rvalid = false;
-                if (Lr != 0) {
-                    k = Lr >= 12 ? rw[0] : 0u;  // block2.go:31-36
-                    v = Lr >= 12 ? rw[1] : 0u;
-                    fn = Lr >= 12 ? rw[2] : 0u;
-                    rvalid = Lr >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)Lr;  // block2.go:57-66
-                    if (rvalid && k >= 8) {  // readKV / DecodeInternalKey (block2.go:38-55)
-                        key_len = k - 8;
-                        if (key_len <= 36) {
-                            uint32_t hh = BHG_FNV_OFFSET;
-#pragma unroll
-                            for (uint32_t t = 3; t < 12; t++)
-#pragma unroll
-                                for (uint32_t b = 0; b < 4; b++) {
-                                    const uint32_t h2 = (hh * BHG_FNV_PRIME) ^ ((rw[t] >> (8 * b)) & 0xffu);
-                                    hh = 4 * (t - 3) + b < key_len ? h2 : hh;
-                                }
-                            fnv = hh;
-                            const uint32_t tb = 12 + key_len, tw = tb >> 2, ts = tb & 3;
-                            uint32_t a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll
-                            for (uint32_t u = 3; u <= 12; u++) {
-                                a0 = tw == u ? rw[u] : a0;
-                                a1 = tw == u ? rw[u + 1] : a1;
-                                if (u + 2 < 14) a2 = tw == u ? rw[u + 2] : a2;
-                            }
-                            trailer = (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, ts) |
-                                      ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, ts) << 32);
-                        } else {
-                            fnv = fnv1_range(pr + 12, key_len, end);
-                            trailer = ldu64(pr + 12 + k - 8, end);
-                        }
-                    }
-                }
-                uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = str;
-                uint64_t dtr = 0;
-                if (Lr != 0) {
-                    dcrc = crc_mask(~acc);  // crc.go:31-33
-                    if (rvalid) {
-                        dk = 12; dkl = key_len; dvo = 12 + k; dvl = v;  // noCompressor.Decode: zero-copy view
-                        dtr = trailer; dfn = fn; dfnv = fnv;
-                        if (expected_crc != nullptr && ri < n && expected_crc[ri] != dcrc) dst = BHG_ST_CRC_MISMATCH;
-                    } else {
-                        dst = BHG_ST_RECORD_NIL;  // ErrBhReadRecordNil
-                    }
-                }
-                uint32_t e0 = dk, e1 = dkl;
-                if (j == 1) { e0 = dvo; e1 = dvl; }
-                if (j == 2) { e0 = (uint32_t)dtr; e1 = (uint32_t)(dtr >> 32); }
-                if (j == 3) { e0 = dfn; e1 = dfnv; }
-                if (j == 4) { e0 = dcrc; e1 = dst; }
-                if (ri < n && j < 5) reinterpret_cast<uint2 *>(out + ri)[j] = make_uint2(e0, e1);
-            }
-        }
-    }
-}
-
-hipError_t launch_decode_tile2(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                               const uint32_t *expected_crc, bhg_desc *out) {
-    constexpr int WPB = 8;
-    const uint64_t tiles = (n + 63) / 64;
-    uint64_t need = (tiles + WPB - 1) / WPB;
-    uint64_t cap = (uint64_t)L.num_cus;  // 148 KiB of LDS: one workgroup per CU
-    uint32_t grid = (uint32_t)(need < cap ? need : cap);
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_tile2<WPB>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
-                       expected_crc, out, L.ztab);
-    return hipGetLastError();
-}
-
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out) {
     constexpr int WPB = 8;  // measured: 12 waves/CU (3 per SIMD) 0.293 ms vs 0.285; non-temporal window loads 0.58 ms

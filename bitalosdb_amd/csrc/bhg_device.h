@@ -1,10 +1,9 @@
 // bhg_device.h -- device-side building blocks for the gfx950 bithash codec.
 //
 // Everything here is integer byte work: no MFMA.  The CRC-32C is table
-// driven out of LDS with the 1 KiB byte table replicated 32x so that lane l
-// always reads bank (l & 31): a random-index lookup by all 64 lanes is then
-// bank-conflict free (ds_read_b32 services lanes in two 32-lane groups, bank
-// = dword address mod 32).  32 KiB of LDS per workgroup.
+// driven out of LDS: slice-by-4 tables replicated R times so that lanes read
+// different banks (ds_read_b32 services lanes in two 32-lane groups, bank =
+// dword address mod 32).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -14,7 +13,6 @@
 #define BHG_CRC_POLY 0x82F63B78u      // Castagnoli, reflected (hash/crc32.Castagnoli)
 #define BHG_FNV_OFFSET 2166136261u    // hash/fnv offset32
 #define BHG_FNV_PRIME 16777619u       // hash/fnv prime32
-#define BHG_CRC_LDS_WORDS (256 * 32)  // replicated table size in dwords
 
 namespace bhg {
 
@@ -43,41 +41,6 @@ __device__ __forceinline__ uint32_t crc_table_entry(uint32_t i) {
     for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ BHG_CRC_POLY : (c >> 1);
     return c;
 }
-
-// Fill the replicated table: dword (i*32 + r) = T[i] for r in 0..31.
-__device__ __forceinline__ void crc_lds_fill(uint32_t *T) {
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-        uint32_t v = crc_table_entry(i);
-        u32x4 v4 = {v, v, v, v};
-        u32x4 *dst = reinterpret_cast<u32x4 *>(T + i * 32);
-#pragma unroll
-        for (int r = 0; r < 8; r++) dst[r] = v4;
-    }
-}
-
-// Per-lane view of the replicated byte table (slice-by-1).
-struct CrcLds {
-    const uint32_t *t;  // T + (lane & 31)
-    __device__ __forceinline__ explicit CrcLds(const uint32_t *T) : t(T + (threadIdx.x & 31)) {}
-    __device__ __forceinline__ uint32_t step(uint32_t c) const { return (c >> 8) ^ t[(c & 0xffu) << 5]; }
-    // absorb one full little-endian word (4 byte steps)
-    __device__ __forceinline__ uint32_t word(uint32_t c, uint32_t w) const {
-        c ^= w;
-        c = step(c); c = step(c); c = step(c); c = step(c);
-        return c;
-    }
-    // absorb the low `nb` (0..4) bytes of x
-    __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const {
-        uint32_t m = nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
-        c ^= x & m;
-#pragma unroll
-        for (uint32_t s = 0; s < 4; s++) {
-            uint32_t n = step(c);
-            c = s < nb ? n : c;
-        }
-        return c;
-    }
-};
 
 // Slice-by-4 tables T0..T3 (T_{k+1}[i] = T_k[i] >> 8 ^ T0[T_k[i] & 0xff]),
 // each replicated R times and interleaved so that lane l reads copy (l % R):
@@ -140,15 +103,6 @@ struct Crc4Lds {
             }
         }
     }
-};
-
-// DIAGNOSTIC ONLY (variant table entries marked diag): a "table" that folds
-// words with xor/rotate instead of CRC lookups -- isolates the memory side of
-// the lane kernels.  Never selected by default; outputs are not CRCs.
-struct XorTab {
-    __device__ __forceinline__ explicit XorTab(const uint32_t *) {}
-    __device__ __forceinline__ uint32_t word(uint32_t c, uint32_t w) const { return ((c << 1) | (c >> 31)) ^ w; }
-    __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const { return word(c, x + nb); }
 };
 
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) {  // crc.go:31-33
@@ -322,141 +276,6 @@ __device__ __forceinline__ uint32_t crc_range_a(const Tab &T, uint32_t c, uint64
     }
     if (pe != pe_all) c = T.partial(c, ld32_safe(pe, end), (uint32_t)(pe_all - pe));
     return c;
-}
-
-// Line-aligned walk with an explicit two-buffer ping-pong (A/B): the loads
-// of window k+1 are issued before window k is absorbed and no register copy
-// joins the buffers, so the compiler's counted s_waitcnt vmcnt(N) keeps the
-// next window in flight (a cur = nxt copy made it wait for everything).
-template <int WIN, class Tab>
-__device__ __forceinline__ uint32_t crc_range_pp(const Tab &T, uint32_t c, uint64_t p, uint64_t len, uint64_t end) {
-    if (len == 0) return c;
-    const uint64_t pe_all = p + len;
-    const uint64_t pa = (p + 3) & ~3ull;
-    if (pa >= pe_all || pa + 4 > pe_all) {
-        uint64_t q = p;
-        while (q < pe_all) {
-            const uint64_t a = q & ~3ull;
-            const uint32_t z = (uint32_t)(q & 3);
-            uint32_t nb = 4 - z;
-            if ((uint64_t)nb > pe_all - q) nb = (uint32_t)(pe_all - q);
-            c = T.partial(c, ld32_safe(a, end) >> (8 * z), nb);
-            q += nb;
-        }
-        return c;
-    }
-    if (pa != p) c = T.partial(c, ld32_safe(p & ~3ull, end) >> (8 * (uint32_t)(p & 3)), (uint32_t)(pa - p));
-    const uint64_t pe = pe_all & ~3ull;
-    constexpr uint32_t WB = 16 * WIN;
-    auto load_win = [&](u32x4 *buf, uint64_t w) {
-        if (w + WB <= end) {
-#pragma unroll
-            for (int q = 0; q < WIN; q++) buf[q] = gld<u32x4_a4>(w + 16 * q);
-        } else {
-#pragma unroll
-            for (int q = 0; q < WIN; q++)
-                buf[q] = u32x4{ld32_safe(w + 16 * q, end), ld32_safe(w + 16 * q + 4, end),
-                               ld32_safe(w + 16 * q + 8, end), ld32_safe(w + 16 * q + 12, end)};
-        }
-    };
-    auto absorb = [&](const u32x4 *buf, uint64_t w) {
-        if (w >= pa && w + WB <= pe) {
-#pragma unroll
-            for (int q = 0; q < WIN; q++) {
-                c = T.word(c, buf[q].x); c = T.word(c, buf[q].y);
-                c = T.word(c, buf[q].z); c = T.word(c, buf[q].w);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < WIN; q++) {
-                const uint64_t b = w + 16 * q;
-                if (b + 0 >= pa && b + 0 < pe) c = T.word(c, buf[q].x);
-                if (b + 4 >= pa && b + 4 < pe) c = T.word(c, buf[q].y);
-                if (b + 8 >= pa && b + 8 < pe) c = T.word(c, buf[q].z);
-                if (b + 12 >= pa && b + 12 < pe) c = T.word(c, buf[q].w);
-            }
-        }
-    };
-    u32x4 A[WIN], Bf[WIN];
-    uint64_t w = pa & ~127ull;
-    if (w < pe) load_win(A, w);
-    while (w < pe) {
-        const uint64_t w1 = w + WB;
-        if (w1 < pe) load_win(Bf, w1);
-        absorb(A, w);
-        if (w1 >= pe) break;
-        const uint64_t w2 = w1 + WB;
-        if (w2 < pe) load_win(A, w2);
-        absorb(Bf, w1);
-        w = w2;
-    }
-    if (pe != pe_all) c = T.partial(c, ld32_safe(pe, end), (uint32_t)(pe_all - pe));
-    return c;
-}
-
-// Buffer-resource walk: windows are read with buffer_load_dwordx4 through a
-// wave-uniform descriptor (base, num_records) whose hardware range check
-// returns 0 past the end instead of faulting, so every load is issued
-// unconditionally (no fast/slow branch, no per-load guard) and the
-// compiler's counted vmcnt keeps window k+1 in flight while k is absorbed.
-// Windows are 128 B line-aligned; head/tail partial words come from the
-// same windows.  `rel` = absolute address - descriptor base (< 2^32).
-template <int WIN, class Tab>
-__device__ __forceinline__ uint32_t crc_range_buf(const Tab &T, uint32_t c, uint64_t p, uint64_t len,
-                                                  __amdgpu_buffer_rsrc_t rsrc, uint64_t rbase, uint32_t nwin_wave,
-                                                  uint64_t rend) {
-    const uint64_t pe_all = p + len;
-    const uint64_t pa = (p + 3) & ~3ull;
-    const uint64_t pe = pe_all & ~3ull;
-    const uint64_t hw = p & ~3ull;                 // head word (partial when p != pa)
-    const uint32_t z = (uint32_t)(p & 3);
-    const uint32_t head_nb = (uint32_t)((pa < pe_all ? pa : pe_all) - p);
-    const uint32_t tail_nb = (uint32_t)(pe_all - pe);
-    const bool has_head = z != 0, has_tail = tail_nb != 0 && pe >= pa;
-    constexpr uint32_t WB = 16 * WIN;
-    const uint64_t w0 = hw & ~(uint64_t)(WB - 1) & ~127ull;
-    const uint32_t o0 = (uint32_t)(w0 - rbase);
-    auto load_win = [&](u32x4 *buf, uint32_t off) {
-#pragma unroll
-        for (int q = 0; q < WIN; q++) buf[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16 * q, 0, 0);
-    };
-    auto absorb = [&](const u32x4 *buf, uint64_t w) {
-        if (w >= pa && w + WB <= pe) {
-#pragma unroll
-            for (int q = 0; q < WIN; q++) {
-                c = T.word(c, buf[q].x); c = T.word(c, buf[q].y);
-                c = T.word(c, buf[q].z); c = T.word(c, buf[q].w);
-            }
-        } else if (w + WB > hw && w < pe_all) {
-#pragma unroll
-            for (int q = 0; q < 4 * WIN; q++) {
-                uint32_t x = q % 4 == 0 ? buf[q / 4].x : q % 4 == 1 ? buf[q / 4].y : q % 4 == 2 ? buf[q / 4].z : buf[q / 4].w;
-                const uint64_t b = w + 4 * q;
-                // a dwordx4 that straddles the descriptor end comes back all-zero: re-read its words
-                if (w + 16 * (q / 4) + 16 > rend && b < rend) x = ld32_safe(b, rend);
-                if (b >= pa && b < pe) c = T.word(c, x);
-                else if (has_head && b == hw) c = T.partial(c, x >> (8 * z), head_nb);
-                else if (has_tail && b == pe) c = T.partial(c, x, tail_nb);
-            }
-        }
-    };
-    u32x4 A[WIN], Bf[WIN];
-    load_win(A, o0);
-    for (uint32_t k = 0; k < nwin_wave; k += 2) {
-        load_win(Bf, o0 + WB * (k + 1));
-        absorb(A, w0 + (uint64_t)WB * k);
-        if (k + 1 >= nwin_wave) break;
-        load_win(A, o0 + WB * (k + 2));
-        absorb(Bf, w0 + (uint64_t)WB * (k + 1));
-    }
-    return c;
-}
-
-// windows a block needs in crc_range_buf
-__device__ __forceinline__ uint32_t crc_buf_windows(uint64_t p, uint64_t len, uint32_t WB) {
-    if (len == 0) return 0;
-    const uint64_t w0 = (p & ~3ull) & ~(uint64_t)(WB - 1) & ~127ull;
-    return (uint32_t)((p + len - w0 + WB - 1) / WB);
 }
 
 template <class Tab>

@@ -31,6 +31,10 @@ struct EncArgs {
     const uint64_t *vlen;         // value' length per record
     uint32_t n;
     const uint32_t *file_nums;
+    const uint32_t *rec_file_nums;  // AddIkey: header fileNum per record (nullable -> file_nums[table])
+    const uint8_t *live;          // compaction liveness mask (nullable -> all live)
+    const uint32_t *khash;        // AddIkey: given khash per record (nullable -> FNV-1 of the key)
+    int single_table;             // AddIkey: one table, no split, dataMaxSize checked per record
     uint32_t max_tables;
     uint32_t init_size;
     uint64_t table_max;
@@ -40,13 +44,27 @@ struct EncArgs {
     bhg_encode_out o;
 };
 
+#define BHG_DATA_MAX_SIZE (0xFFFFFFFFull - (256ull << 20))  // writer.go:45
+
+// the add of record i (status OK after k_enc_sizes, position P, length L)
+// lands in the output: out_cap for every batch, dataMaxSize (writer.go:266-269)
+// for the single-table AddIkey batch (the split batch rejects table_max values
+// that could reach it up front)
+__device__ __forceinline__ uint32_t fit_status(const EncArgs &a, uint64_t P, uint32_t L) {
+    if (P + L > a.out_cap) return BHG_ST_NO_SPACE;
+    if (a.single_table && (uint64_t)a.init_size + P + L > BHG_DATA_MAX_SIZE) return BHG_ST_DATA_MAX_EXCEEDED;
+    return BHG_ST_OK;
+}
+
 __global__ __launch_bounds__(256) void k_enc_sizes(EncArgs a) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
         const uint64_t klen = a.key_off[i + 1] - a.key_off[i];
         const uint64_t vl = a.vlen[i];
         uint32_t st = BHG_ST_OK;
         uint64_t L = 0;
-        if (klen + 8 > BHG_MAX_KEY_SIZE) st = BHG_ST_KEY_TOO_LARGE;
+        if (a.live != nullptr && a.live[i] == 0) st = BHG_ST_SKIPPED;           // bitree/bithash.go:225-228
+        else if (klen + 8 > BHG_MAX_KEY_SIZE) st = BHG_ST_KEY_TOO_LARGE;
+        else if (vl == ~0ull) st = BHG_ST_NO_SPACE;                              // snappy scratch overflow
         else if (vl > BHG_MAX_VALUE_SIZE) st = BHG_ST_VALUE_TOO_LARGE;
         else L = 12 + klen + 8 + vl;
         a.o.status[i] = st;
@@ -89,7 +107,8 @@ __global__ __launch_bounds__(1024) void k_enc_split(EncArgs a) {
     uint32_t s = 0, t = 0, fail = 0;
     uint64_t S = a.init_size;
     if (threadIdx.x == 0) a.o.table_start[0] = 0;
-    while (s < n) {
+    // BithashWriter.AddIkey never splits (bithash_writer.go:43-45)
+    while (!a.single_table && s < n) {
         const uint64_t T = a.table_max > S ? pos[s] + (a.table_max - S) : pos[s];
         uint32_t e = first_geq(pos, s, n, T, &s_best);
         while (e < n && pos[e + 1] == pos[e]) e++;     // split check runs only after a successful add
@@ -139,11 +158,11 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
         if (a.o.status[r] != BHG_ST_OK) continue;
         const uint64_t P = a.lens[r];
         const uint32_t L = (uint32_t)(a.lens[r + 1] - P);
-        if (P + L > a.out_cap) continue;
+        if (fit_status(a, P, L) != BHG_ST_OK) continue;
         const uint32_t klen = (uint32_t)(a.key_off[r + 1] - a.key_off[r]);
         const uint32_t vl = (uint32_t)a.vlen[r];
         const uint32_t t = table_of(a.o.table_start, ntab, r);
-        const uint32_t fn = a.file_nums[t];
+        const uint32_t fn = a.rec_file_nums != nullptr ? a.rec_file_nums[r] : a.file_nums[t];
         const uint64_t kp = (uint64_t)a.keys + a.key_off[r];
         const uint64_t trailer = a.trailers[r];
         const uint64_t vp = (uint64_t)a.vals + a.vpos[r];
@@ -200,15 +219,21 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
     const Crc4Lds<R> crc(T);
     const uint32_t ntab = (uint32_t)a.o.summary[1];
     const uint64_t out_end = (uint64_t)a.out + a.out_cap;
+    uint32_t failed = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
         const uint64_t kp = (uint64_t)a.keys + a.key_off[i];
         const uint32_t klen = (uint32_t)(a.key_off[i + 1] - a.key_off[i]);
-        a.o.fnv1[i] = fnv1_range(kp, klen, kp + klen);   // writer.go:246 (every Add, before add())
+        // writer.go:246 (Add: FNV-1 of every key, before add()) / :249 (AddIkey: the caller's khash)
+        a.o.fnv1[i] = a.khash != nullptr ? a.khash[i] : fnv1_range(kp, klen, kp + klen);
         const uint32_t t = ntab ? table_of(a.o.table_start, ntab, i) : 0;
         a.o.table[i] = t;
         const uint64_t P = a.lens[i];
         const uint32_t L = (uint32_t)(a.lens[i + 1] - P);
-        if (a.o.status[i] != BHG_ST_OK || ntab == 0 || P + L > a.out_cap) {
+        uint32_t st = a.o.status[i];
+        if (st == BHG_ST_OK) st = ntab != 0 ? fit_status(a, P, L) : BHG_ST_NO_SPACE;  // ntab 0: out of file_nums
+        if (st != BHG_ST_OK) {
+            if (st != a.o.status[i]) a.o.status[i] = st;
+            failed += st != BHG_ST_SKIPPED;
             a.o.pos[i] = ~0ull;
             a.o.bh_off[i] = 0;
             a.o.bh_len[i] = 0;
@@ -221,6 +246,10 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
         a.o.bh_len[i] = L;
         a.o.crc[i] = crc_mask(~crc_range_a<8>(crc, 0xffffffffu, (uint64_t)a.out + P, L, out_end));
     }
+    // summary[2]: failed adds (every status but OK / SKIPPED); one vector atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) failed += __shfl_xor(failed, d);
+    if ((threadIdx.x & 63) == 0 && failed) atomicAdd(reinterpret_cast<unsigned long long *>(a.o.summary + 2),
+                                                     (unsigned long long)failed);
 }
 
 // value' = raw values: vpos = val_off, vlen = val_off[i+1]-val_off[i]
@@ -233,7 +262,8 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     EncArgs a;
     a.keys = E.keys; a.key_off = E.key_off; a.trailers = E.trailers;
     a.vals = E.vbase; a.vpos = E.vpos; a.vlen = E.vlen;
-    a.n = E.n; a.file_nums = E.file_nums; a.max_tables = E.max_tables; a.init_size = E.init_size;
+    a.n = E.n; a.file_nums = E.file_nums; a.rec_file_nums = E.rec_file_nums; a.live = E.live; a.khash = E.khash;
+    a.single_table = E.single_table; a.max_tables = E.max_tables; a.init_size = E.init_size;
     a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
     const uint32_t g = lane_grid(L, E.n, 256);
     hipLaunchKernelGGL(k_enc_sizes, dim3(g), dim3(256), 0, L.stream, a);

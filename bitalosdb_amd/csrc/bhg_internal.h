@@ -1,5 +1,5 @@
 // bhg_internal.h -- host-side glue shared by the kernel translation units
-// and the C-ABI implementation (bhg_api.cpp).  Not part of the public ABI.
+// and the C-ABI implementation (bhg_api.hip).  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -10,42 +10,36 @@ namespace bhg {
 
 struct Launch {
     hipStream_t stream;
-    int num_cus;        // 256 on MI355X
-    int lane_wgs_per_cu;  // override of resident workgroups per CU (0 = variant default)
-    int variant;          // lane-kernel variant (bhg_decode.hip kLaneVariants)
-    int snappy_variant;   // 0: lane-per-block snappy decode, 1: wave-per-block, 2: lane, one round trip per element
-    const uint32_t *ztab; // device copy of build_tile_ztab() (owned by the context)
+    int num_cus;           // 256 on MI355X
+    const uint32_t *ztab;  // device copy of build_tile_ztab() (owned by the context)
+    const uint32_t *stab;  // device copy of build_stream_tab(128, 4) (owned by the context)
 };
 
-// persistent grid for lane-per-block kernels: enough workgroups to fill the
-// chip (LDS-limited residency), never more than the work needs
+// persistent grid for lane-per-item kernels: enough workgroups to fill the
+// chip, never more than the work needs
 inline uint32_t lane_grid(const Launch &L, uint64_t n, uint32_t block) {
     uint64_t need = (n + block - 1) / block;
-    uint64_t cap = (uint64_t)L.num_cus * (uint64_t)(L.lane_wgs_per_cu > 0 ? L.lane_wgs_per_cu : 4);
+    uint64_t cap = (uint64_t)L.num_cus * 4;
     uint64_t g = need < cap ? need : cap;
     return g == 0 ? 1u : (uint32_t)g;
 }
 
-// bhg_decode.hip
-hipError_t launch_decode_lane(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                              int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
-// bhg_decode_tile.hip: default NoCompressor decode (variant kTileVariant)
-constexpr int kTileVariant = 44;
+// bhg_decode.hip: descriptors for codec NONE (complete) or the snappy header
+// pass (sizes[i] = decoded length; the values follow with launch_snappy)
+hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+// bhg_decode_tile.hip: the NoCompressor decode kernel
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out);
-// k_decode_tile2 (variant kTile2Variant): no lane-per-record phase, W = 144 B windows
-constexpr int kTile2Variant = 45;
-hipError_t launch_decode_tile2(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                               const uint32_t *expected_crc, bhg_desc *out);
-hipError_t launch_snappy_wave(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                              bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
-// bhg_snappy_dec.hip: lane-per-block snappy decode, one memory round trip per element (snappy_variant 2)
-hipError_t launch_snappy_rt(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                            bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
-                            bool win = false);  // win: tag stream through a per-lane LDS window (snappy_variant 4)
-// bhg_snappy_dec.hip: group-of-8-lanes snappy decode staged in LDS (snappy_variant 3)
-hipError_t launch_snappy_grp(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                             bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
+// bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
+// the shift tables it reads (Launch::stab) are built on the host once per context
+size_t stream_tab_words();
+void build_stream_tab_default(uint32_t *out);
+hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+// bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
+hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                         bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off);
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)
@@ -68,7 +62,11 @@ struct EncodeLaunch {
     const uint64_t *vpos;      // value' offsets into vbase
     const uint64_t *vlen;      // value' lengths
     uint32_t n;
-    const uint32_t *file_nums;
+    const uint32_t *file_nums;      // per table
+    const uint32_t *rec_file_nums;  // per record (AddIkey), nullable
+    const uint8_t *live;            // per record liveness (compaction), nullable
+    const uint32_t *khash;          // per record given khash (AddIkey), nullable -> FNV-1 of the key
+    int single_table;               // AddIkey: one table, no split; dataMaxSize checked per record
     uint32_t max_tables;
     uint32_t init_size;
     uint64_t table_max;
@@ -84,8 +82,10 @@ hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t
 // bhg_snappy_enc.hip
 hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *out);
 uint32_t snappy_enc_grid(const Launch &L, uint32_t n);
+// values whose MaxEncodedLen slot would end past scap get clen = ~0 (-> BHG_ST_NO_SPACE)
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
-                             uint8_t *scratch, const uint64_t *soff, uint64_t *clen, uint16_t *gtables);
+                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
+                             uint16_t *gtables);
 
 // bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
 // scratch must hold scan_scratch_bytes(n).

@@ -240,7 +240,7 @@ rem:
 
 // one wave per value: val bytes vals[val_off[i] .. val_off[i+1]) -> scratch[soff[i] ..), clen[i]
 __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
-                                                   uint32_t n, uint8_t *__restrict__ scratch,
+                                                   uint32_t n, uint8_t *__restrict__ scratch, uint64_t scap,
                                                    const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
                                                    uint16_t *__restrict__ gtables) {
     __shared__ __attribute__((aligned(16))) uint8_t in[SE_CAP + 16];
@@ -251,6 +251,10 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
     uint16_t *gt = gtables + (size_t)blockIdx.x * 16384;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
+        if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
+            if (lane == 0) clen[i] = ~0ull;
+            continue;
+        }
         const uint8_t *src = vals + v0;
         Out o;
         o.g = scratch + soff[i];
@@ -313,9 +317,10 @@ uint32_t snappy_enc_grid(const Launch &L, uint32_t n) {
 }
 
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
-                             uint8_t *scratch, const uint64_t *soff, uint64_t *clen, uint16_t *gtables) {
+                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
+                             uint16_t *gtables) {
     hipLaunchKernelGGL(k_snappy_enc, dim3(snappy_enc_grid(L, n)), dim3(64), 0, L.stream, vals, val_off, n, scratch,
-                       soff, clen, gtables);
+                       scap, soff, clen, gtables);
     return hipGetLastError();
 }
 

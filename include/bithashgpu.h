@@ -18,14 +18,18 @@
  * pointer is DEVICE memory (device-resident path); *_host variants take
  * host memory and include the H2D/D2H copies (end-to-end path).
  *
- * Ownership: the library never frees caller memory.  Device scratch is owned
- * by the bhg_ctx.  Errors: functions return 0 (BHG_OK) or a negative
+ * Ownership: the library never frees caller memory.  Device scratch is
+ * allocated per call from the context's stream-ordered memory pool and freed
+ * on the call's stream after its last kernel (hipMallocFromPoolAsync /
+ * hipFreeAsync), so concurrent calls never share scratch.  Errors: functions return 0 (BHG_OK) or a negative
  * BHG_E* code; bhg_last_error() gives the text.  Nothing aborts or throws
  * across this boundary.  Per-block outcomes are reported in status columns
  * (BHG_ST_*), mapped 1:1 onto the reference's Go errors.
  *
  * Threading: a bhg_ctx may be used from several host threads on distinct
- * streams; calls on one stream are ordered.  Multi-GPU: one ctx per device.
+ * streams; calls on one stream are ordered.  The *_host entry points are
+ * synchronous and serialise on the context (they own its staging buffers).
+ * Multi-GPU: one ctx per device.
  */
 #ifndef BITHASHGPU_H
 #define BITHASHGPU_H
@@ -37,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BHG_ABI_VERSION 1
+#define BHG_ABI_VERSION 2
 
 /* ---- API return codes ---- */
 #define BHG_OK 0
@@ -63,6 +67,10 @@ extern "C" {
 #define BHG_ST_VALUE_TOO_LARGE 8   /* ErrBhValueTooLarge (writer.go:262-263) */
 #define BHG_ST_DATA_MAX_EXCEEDED 9 /* "bithash: panic add exceed data max size" (writer.go:266-269) */
 #define BHG_ST_NOT_FOUND 10        /* HashIndex miss: ErrBhNotFound (reader.go:210-213) */
+#define BHG_ST_NO_SPACE 11         /* encode: the record does not fit in out_cap (or max_tables ran out);
+                                      nothing was written for it -- grow the buffer and re-run */
+#define BHG_ST_SKIPPED 12          /* encode: live[i] == 0, the compaction filter dropped the record
+                                      (bitree/bithash.go:225-228); not an error */
 
 /* BlockHandle (block.go:26-39) with the offset widened to 64 bits so one
  * batch may span many concatenated/mmap'd table files. 16 B. */
@@ -136,8 +144,13 @@ int bhg_memset_device(bhg_ctx *ctx, void *dst, int value, uint64_t bytes, void *
  *   out_val_off[n+1] : written by the library: exclusive scan of the decoded
  *                      lengths; out_val_off[n] = total bytes needed
  *   out_vals, out_vals_cap : decoded values; a block whose slot would end past
- *                      out_vals_cap gets BHG_ST_SNAPPY_TOO_LARGE
- * Asynchronous on `stream`.  All pointers device memory. */
+ *                      out_vals_cap gets BHG_ST_SNAPPY_TOO_LARGE.
+ *                      out_vals NULL = sizing pass: only the header/CRC pass
+ *                      and the scan run; descriptors then hold the header
+ *                      pass's provisional val_off (compressed payload offset
+ *                      in the record) and val_len (decoded length).
+ * Asynchronous on `stream` (no host synchronisation inside).  All pointers
+ * device memory. */
 int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                      uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                      uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off, void *stream);
@@ -147,7 +160,9 @@ int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const b
  * is the end-to-end path (mmap'd .bht -> H2D -> kernel -> D2H).  For codec
  * NONE with handles sorted by offset (table scans, compaction) the batch is
  * pipelined in <= 64 MiB chunks over 3 streams, so H2D, kernels and D2H
- * overlap; otherwise src is copied whole first. */
+ * overlap; otherwise src is copied whole first.  SNAPPY: the device value
+ * buffer is sized from the scanned total (not from out_vals_cap); out_vals
+ * NULL returns only out_val_off (the sizing pass). */
 int bhg_decode_batch_host(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                           uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                           uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off);
@@ -182,13 +197,18 @@ int bhg_fnv32_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bh
  *   keys, key_off[n+1]      : concatenated user keys
  *   trailers[n]             : ikey trailers (seq<<8 | kind)
  *   vals, val_off[n+1]      : concatenated raw values
+ *   vals_len                : val_off[n] (host-known total, sizes the snappy
+ *                             scratch without a device read; values whose
+ *                             encoding would overflow it get BHG_ST_NO_SPACE)
  *   codec                   : BHG_CODEC_NONE / BHG_CODEC_SNAPPY (golang/snappy v0.0.4 Encode)
  *   file_nums[max_tables]   : fileNum of table 0,1,2... (header fileNum of its records)
  *   init_size               : meta.Size/currentOffset of table 0 when the batch starts
  *   table_max               : TableMaxSize; after each successful add,
  *                             size >= table_max starts the next table at 0
- *   out, out_cap            : packed records of all tables, concatenated
- * Outputs (device arrays, n entries unless noted) in bhg_encode_out. */
+ *   out, out_cap            : packed records of all tables, concatenated;
+ *                             records ending past out_cap get BHG_ST_NO_SPACE
+ * Outputs (device arrays, n entries unless noted) in bhg_encode_out.
+ * Asynchronous on `stream` (no host synchronisation inside). */
 typedef struct bhg_encode_out {
     uint64_t *pos;          /* byte position of record i in out (UINT64_MAX if its add failed) */
     uint32_t *bh_off;       /* BlockHandle.Offset inside its table */
@@ -196,15 +216,40 @@ typedef struct bhg_encode_out {
     uint32_t *table;        /* table index (0-based) */
     uint32_t *fnv1;         /* hash.Fnv32(userKey) */
     uint32_t *crc;          /* masked CRC-32C of the packed record */
-    uint32_t *status;       /* BHG_ST_OK / KEY_TOO_LARGE / VALUE_TOO_LARGE / DATA_MAX_EXCEEDED */
+    uint32_t *status;       /* BHG_ST_OK / KEY_TOO_LARGE / VALUE_TOO_LARGE / DATA_MAX_EXCEEDED /
+                               NO_SPACE / SKIPPED */
     uint32_t *table_start;  /* [max_tables] first record index of each table */
-    uint64_t *summary;      /* [4]: total bytes written, tables used, failed adds, reserved */
+    uint64_t *summary;      /* [4]: bytes the batch occupies in out (out_cap >= this
+                               writes every record), tables used (0 = max_tables too
+                               small), failed adds (status not OK/SKIPPED), split failed */
 } bhg_encode_out;
 
 int bhg_encode_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
-                     const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                     const uint8_t *vals, const uint64_t *val_off, uint64_t vals_len, uint32_t n, int codec,
                      const uint32_t *file_nums, uint32_t max_tables, uint32_t init_size, uint64_t table_max,
                      uint8_t *out, uint64_t out_cap, const bhg_encode_out *o, void *stream);
+
+/* ---- compaction re-pack (device): BithashWriter.AddIkey over N records ----
+ * Replaces the per-record loop of compactBithashFiles (bitree/bithash.go:217-239):
+ * the liveness filter (findKey -> skip) and bw.AddIkey(ik, v, khash, fn)
+ * (bithash_writer.go:43-45, writer.go:249-255): the value bytes are written
+ * as given (already encoded: TableIterator hands out stored bytes), the
+ * header fileNum is the record's SOURCE file, the khash is the caller's, and
+ * all records go to ONE table (AddIkey never calls maybeSplitTable).
+ *   keys/key_off/trailers/vals/val_off : as bhg_encode_batch (vals = stored value bytes)
+ *   khash[n]        : nullable -> hash.Fnv32(userKey)
+ *   rec_file_nums[n]: header fileNum of each record
+ *   live[n]         : nullable u8 mask; 0 -> BHG_ST_SKIPPED, no bytes, no handle
+ *   init_size       : the destination writer's currentOffset when the batch starts
+ *   out, out_cap, o : as bhg_encode_batch; o->table_start needs 1 entry, table[] is 0.
+ * Statuses: OK, SKIPPED, KEY_TOO_LARGE, VALUE_TOO_LARGE, DATA_MAX_EXCEEDED
+ * (writer.go:266-269, per record against init_size + position), NO_SPACE.
+ * The reference aborts the compaction at its first failed add; a caller
+ * mirroring it stops at the first status not OK/SKIPPED. */
+int bhg_encode_ikey_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                          const uint8_t *vals, const uint64_t *val_off, uint32_t n, const uint32_t *khash,
+                          const uint32_t *rec_file_nums, const uint8_t *live, uint32_t init_size, uint8_t *out,
+                          uint64_t out_cap, const bhg_encode_out *o, void *stream);
 
 /* ---- table data-region scan (device) ----
  * TableIterator.findEntry (bithash/table.go:358-395, mode 0) or Writer.rebuild

@@ -20,6 +20,7 @@ assert HANDLE_DT.itemsize == 16 and DESC_DT.itemsize == 40
 
 OK, RECORD_NIL, ILLEGAL_LENGTH, INCOMPLETE, SNAPPY_CORRUPT, SNAPPY_TOO_LARGE, CRC_MISMATCH = range(7)
 KEY_TOO_LARGE, VALUE_TOO_LARGE, DATA_MAX_EXCEEDED = 7, 8, 9
+NOT_FOUND, NO_SPACE, SKIPPED = 10, 11, 12  # include/bithashgpu.h (encode-side statuses of the C-ABI)
 
 _lib = None
 

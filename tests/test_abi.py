@@ -20,7 +20,7 @@ def test_library_builds_and_loads():
     B.build()
     assert os.path.exists(B.LIB_PATH)
     L = B.lib()
-    assert L.bhg_abi_version() == 1
+    assert L.bhg_abi_version() == B.ABI_VERSION == 2
 
 
 def test_exports_match_header():
@@ -56,3 +56,16 @@ def test_no_device_means_no_context():
     L = B.lib()
     assert L.bhg_device_count() == 0
     assert not L.bhg_create(0, 0)
+
+
+def test_no_selectable_kernel_variants():
+    """The shipped library has one kernel per job: no environment switch can
+    select an exploration or diagnostic kernel (those live in scripts/lab)."""
+    B.build()
+    blob = open(B.LIB_PATH, "rb").read()
+    for env in (b"BHG_DECODE_VARIANT", b"BHG_SNAPPY_VARIANT", b"BHG_LANE_WGS_PER_CU", b"BHG_HOST_NOPIPE"):
+        assert env not in blob, env
+    syms = subprocess.check_output(["nm", "-C", B.LIB_PATH]).decode()
+    for k in ("k_diag", "k_decode_lane", "k_decode_coop", "k_decode_lanebuf", "k_snappy_wave", "k_decode_tile2"):
+        assert k not in syms, k
+    assert not re.search(rb"BHG_[A-Z_]*VARIANT", blob)

@@ -21,23 +21,10 @@ pytestmark = pytest.mark.gpu
 FIELDS = ["key_off", "key_len", "val_off", "val_len", "trailer", "file_num", "fnv1", "crc", "status"]
 
 
-@pytest.fixture(scope="module", params=["44", "45"], ids=["tile", "tile2"])
-def codec(request):
-    """Every test runs once per NoCompressor tile kernel (k_decode_tile,
-    k_decode_tile2); the variant is read when the context is created."""
-    import os
-    from bitalosdb_amd import _lib
+@pytest.fixture(scope="module")
+def codec():
     from bitalosdb_amd.codec import BithashCodec
-    _lib.lib()
-    old = os.environ.get("BHG_DECODE_VARIANT")
-    os.environ["BHG_DECODE_VARIANT"] = request.param
-    try:
-        c = BithashCodec(0)
-    finally:
-        if old is None:
-            os.environ.pop("BHG_DECODE_VARIANT")
-        else:
-            os.environ["BHG_DECODE_VARIANT"] = old
+    c = BithashCodec(0)
     yield c
     c.close()
 
@@ -285,22 +272,6 @@ def _full_size(codec, synth, handles_tensor, n):
     assert (got["trailer"] >> 8 == np.arange(1, n + 1)).all()
 
 
-@pytest.mark.parametrize("variant", [v for v in range(46) if v not in (17, 18, 19, 25, 26, 27, 29, 31, 32, 36)])
-def test_lane_kernel_variants(variant, monkeypatch):
-    """Every CRC-table flavour of k_decode_lane is bit-exact (slice-by-1/4, R=4..32)."""
-    from bitalosdb_amd.codec import BithashCodec
-    monkeypatch.setenv("BHG_DECODE_VARIANT", str(variant))
-    c = BithashCodec(0)
-    rng = random.Random(100 + variant)
-    specs = [(rand_bytes(rng, rng.choice([0, 7, 32])), rand_bytes(rng, rng.choice([1, 3, 64, 1024, 2047])), 5)
-             for _ in range(2000)]
-    src, h = make_records(rng, specs, gap_max=3)
-    got, _, _ = c.decode(src, h)
-    exp, _, _ = O.decode_batch(src, h)
-    assert_desc_equal(got, exp)
-    c.close()
-
-
 def test_tile_window_edges(codec):
     """Record lengths around the 144-B / 128-B window grid of the tile kernels:
     heads of 1..4 bytes, exactly 8 / 9 / 17 windows, records of 1..3 bytes
@@ -328,13 +299,12 @@ def test_tile_window_edges(codec):
     assert_desc_equal(got, exp)
 
 
-@pytest.mark.parametrize("sv", [0, 1, 2, 3, 4])
-def test_snappy_kernel_variants(sv, monkeypatch):
-    """lane-per-block and wave-per-block snappy decoders are both bit-exact."""
-    from bitalosdb_amd.codec import BithashCodec
-    monkeypatch.setenv("BHG_SNAPPY_VARIANT", str(sv))
-    c = BithashCodec(0)
-    rng = random.Random(300 + sv)
+@pytest.mark.parametrize("seed", [0, 1])
+def test_snappy_value_shapes(codec, seed):
+    """Snappy values of every element shape the decoder distinguishes: short
+    and long literals, copies with offset < length (LZ77 overlap, periods
+    1..3), incompressible values, a 70 KiB value (several 64 KiB blocks)."""
+    rng = random.Random(300 + seed)
     specs = []
     for i in range(1500):
         vl = rng.choice([1, 3, 15, 16, 17, 31, 64, 100, 1024, 1024, 3000, 5000, 70000 if i % 500 == 0 else 2000])
@@ -343,11 +313,117 @@ def test_snappy_kernel_variants(sv, monkeypatch):
             (b"a" * vl) if kind == 2 else rand_bytes(rng, vl)
         specs.append((rand_bytes(rng, 32), v, 2))
     src, h = make_records(rng, specs, gap_max=5, codec=1)
-    got, gv, go = c.decode(src, h, compressor=1)
+    got, gv, go = codec.decode(src, h, compressor=1)
     exp, ev, eo = O.decode_batch(src, h, codec=1)
     assert_desc_equal(got, exp)
     assert np.array_equal(go, eo) and gv.tobytes() == ev[:int(eo[-1])].tobytes()
-    c.close()
+
+
+def test_snappy_sizing_pass_and_small_cap(codec):
+    """out_vals NULL = sizing pass (scan only, provisional descriptors); an
+    out_vals_cap below the total gives SNAPPY_TOO_LARGE exactly to the blocks
+    whose slot ends past it, the others decode normally."""
+    from bitalosdb_amd.codec import as_device_bytes, handles_tensor
+    rng = random.Random(41)
+    specs = [(rand_bytes(rng, 16), compressible(rng, rng.choice([10, 500, 1024, 4000])), 3) for _ in range(400)]
+    src, h = make_records(rng, specs, codec=1)
+    exp, ev, eo = O.decode_batch(src, h, codec=1)
+    with torch.cuda.stream(codec.stream):
+        st = as_device_bytes(src, codec.device)
+        ht = handles_tensor(h, codec.device)
+        probe = codec.decode_batch(st, st.numel(), ht, len(h), 1)
+        codec.sync()
+        assert np.array_equal(probe.val_off_np(), eo)
+        pd = probe.desc_np()
+        assert (pd["status"] == 0).all()
+        assert np.array_equal(pd["val_len"], exp["val_len"])       # provisional: decoded length
+        cap = int(eo[250]) + 7                                      # blocks 250.. end past cap
+        vals = torch.zeros(cap, dtype=torch.uint8, device=codec.device)
+        res = codec.decode_batch(st, st.numel(), ht, len(h), 1, out_vals=vals)
+        codec.sync()
+    d = res.desc_np()
+    ends = eo[1:]
+    assert (d["status"][ends > cap] == O.SNAPPY_TOO_LARGE).all()
+    ok = ends <= cap
+    assert (d["status"][ok] == 0).all()
+    for f in FIELDS:
+        assert np.array_equal(d[f][ok], exp[f][ok]), f
+    assert vals.cpu().numpy()[:int(eo[250])].tobytes() == ev[:int(eo[250])].tobytes()
+    # host path: exact sizing and a small cap
+    d2, v2, o2 = codec.decode_host(src, h, compressor=1)
+    assert_desc_equal(d2, exp)
+    assert v2.tobytes() == ev[:int(eo[-1])].tobytes()
+    d3, v3, _ = codec.decode_host(src, h, compressor=1, out_vals_cap=cap)
+    assert (d3["status"][ends > cap] == O.SNAPPY_TOO_LARGE).all() and (d3["status"][ok] == 0).all()
+    assert v3[:int(eo[250])].tobytes() == ev[:int(eo[250])].tobytes()
+
+
+def test_two_threads_two_streams(codec):
+    """One context, two host threads, each on its own HIP stream, running
+    snappy decode (per-call scan scratch) and encode (per-call scratch)
+    concurrently many times: every result equals the restatement."""
+    import threading
+    from bitalosdb_amd.codec import as_device_bytes, handles_tensor, _u64_tensor, _u32_tensor, EncodeBuffers
+    rng = random.Random(55)
+    specs = [(rand_bytes(rng, 24), compressible(rng, rng.choice([100, 1024, 3000])), 2) for _ in range(2000)]
+    src, h = make_records(rng, specs, codec=1)
+    exp, ev, eo = O.decode_batch(src, h, codec=1)
+    keys = [rand_bytes(rng, 20) for _ in range(1500)]
+    vals = [compressible(rng, rng.choice([64, 700, 2048])) for _ in range(1500)]
+    trs = [(i + 1) << 8 | 1 for i in range(1500)]
+    eexp = O.encode_batch(keys, trs, vals, codec=1, file_nums=[1, 2, 3, 4], table_max=1 << 20)
+    errors = []
+    dev = codec.device
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    with torch.cuda.stream(streams[0]):
+        st = as_device_bytes(src, dev)
+        ht = handles_tensor(h, dev)
+    with torch.cuda.stream(streams[1]):
+        ko = np.zeros(len(keys) + 1, np.uint64); np.cumsum([len(k) for k in keys], out=ko[1:])
+        vo = np.zeros(len(vals) + 1, np.uint64); np.cumsum([len(v) for v in vals], out=vo[1:])
+        kb = as_device_bytes(b"".join(keys), dev); vb = as_device_bytes(b"".join(vals), dev)
+        kot, vot, trt = _u64_tensor(ko, dev), _u64_tensor(vo, dev), _u64_tensor(trs, dev)
+        fns = _u32_tensor([1, 2, 3, 4], dev)
+    torch.cuda.synchronize()
+
+    def dec_worker():
+        try:
+            s = streams[0]
+            with torch.cuda.stream(s):
+                for _ in range(8):
+                    vals_t = torch.zeros(int(eo[-1]), dtype=torch.uint8, device=dev)
+                    off_t = torch.empty((len(h) + 1) * 8, dtype=torch.uint8, device=dev)
+                    res = codec.decode_batch(st, st.numel(), ht, len(h), 1, out_vals=vals_t, out_val_off=off_t,
+                                             stream=s.cuda_stream)
+                    s.synchronize()
+                    assert np.array_equal(res.val_off_np(), eo)
+                    assert vals_t.cpu().numpy().tobytes() == ev[:int(eo[-1])].tobytes()
+                    assert np.array_equal(res.desc_np()["crc"], exp["crc"])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def enc_worker():
+        try:
+            s = streams[1]
+            with torch.cuda.stream(s):
+                for _ in range(8):
+                    out = torch.zeros(int(vo[-1]) * 2 + 64 * len(keys), dtype=torch.uint8, device=dev)
+                    bufs = EncodeBuffers(len(keys), 4, dev)
+                    codec.encode_batch(kb, kot, trt, vb, vot, len(keys), 1, fns, 4, 0, 1 << 20, out, bufs,
+                                       stream=s.cuda_stream, vals_len=int(vo[-1]))
+                    s.synchronize()
+                    total = int(bufs.summary.cpu().numpy()[0])
+                    assert out[:total].cpu().numpy().tobytes() == eexp["out"].tobytes()
+                    assert np.array_equal(bufs.crc.cpu().numpy().view(np.uint32), eexp["crc"])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=dec_worker), threading.Thread(target=enc_worker)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
 
 
 @pytest.mark.parametrize("chunk,big", [(4096, False), (1 << 20, False), (4096, True)])

@@ -139,3 +139,114 @@ def test_encode_snappy_byte_exact(codec, seed):
     assert (desc["status"] == 0).all()
     for i in range(0, n, 37):
         assert dv[int(doff[i]):int(doff[i + 1])].tobytes() == vals[i]
+
+
+def test_encode_out_cap_too_small(codec):
+    """Records that end past out_cap are not written: status NO_SPACE, pos
+    UINT64_MAX, counted in summary[2]; summary[0] still reports the bytes the
+    whole batch needs; everything before the cut equals the restatement."""
+    rng = random.Random(21)
+    n = 1000
+    keys = [rb(rng, 16) for _ in range(n)]
+    vals = [rb(rng, rng.choice([10, 300, 1000])) for _ in range(n)]
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    exp = O.encode_batch(keys, tr, vals, file_nums=[1, 2], table_max=64 << 20)
+    cap = int(exp["pos"][600]) + 5
+    got = codec.encode(keys, tr, vals, file_nums=[1, 2], table_max=64 << 20, out_cap=cap)
+    fits = exp["pos"] + exp["bh_len"] <= cap
+    assert fits[:600].all() and not fits[600:].any()
+    assert (got["status"][fits] == 0).all() and (got["status"][~fits] == O.NO_SPACE).all()
+    assert (got["pos"][~fits] == np.iinfo(np.uint64).max).all()
+    assert int(got["summary"][2]) == int((~fits).sum())
+    assert int(got["summary"][0]) == len(exp["out"])
+    for f in ("fnv", "bh_off", "bh_len", "crc", "pos"):
+        assert np.array_equal(got[f][fits], exp[f][fits]), f
+    assert got["out"][:int(exp["pos"][600])].tobytes() == exp["out"][:int(exp["pos"][600])].tobytes()
+
+
+def test_encode_snappy_vals_len_too_small(codec):
+    """A vals_len below val_off[n] cannot overflow the snappy scratch: the
+    values past the bound get NO_SPACE, the rest encode exactly."""
+    import torch
+    from bitalosdb_amd.codec import EncodeBuffers, as_device_bytes, _u32_tensor, _u64_tensor
+    rng = random.Random(22)
+    n = 300
+    keys = [rb(rng, 8) for _ in range(n)]
+    vals = [compressible(rng, 1000) for _ in range(n)]
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    exp = O.encode_batch(keys, tr, vals, codec=1, file_nums=[3], table_max=64 << 20)
+    dev = codec.device
+    with torch.cuda.stream(codec.stream):
+        ko = np.zeros(n + 1, np.uint64); np.cumsum([len(k) for k in keys], out=ko[1:])
+        vo = np.zeros(n + 1, np.uint64); np.cumsum([len(v) for v in vals], out=vo[1:])
+        out = torch.zeros(len(exp["out"]) + 64, dtype=torch.uint8, device=dev)
+        bufs = EncodeBuffers(n, 1, dev)
+        codec.encode_batch(as_device_bytes(b"".join(keys), dev), _u64_tensor(ko, dev), _u64_tensor(tr, dev),
+                           as_device_bytes(b"".join(vals), dev), _u64_tensor(vo, dev), n, 1, _u32_tensor([3], dev),
+                           1, 0, 64 << 20, out, bufs, vals_len=int(vo[-1]) // 2)
+        codec.sync()
+    st = bufs.status.cpu().numpy().view(np.uint32)
+    assert (st[:100] == 0).all() and (st[-50:] == O.NO_SPACE).all()
+    ok = st == 0
+    first_bad = int(np.argmin(ok))
+    assert ok[:first_bad].all() and not ok[first_bad:].any()
+    crc = bufs.crc.cpu().numpy().view(np.uint32)
+    assert np.array_equal(crc[:first_bad], exp["crc"][:first_bad])
+
+
+@pytest.mark.parametrize("codec_kind", [0, 1])
+def test_encode_ikey_compaction_repack(codec, codec_kind):
+    """Compaction re-pack (bitree/bithash.go:217-239): source tables scanned
+    and decoded on the GPU (stored value bytes, source fileNum), a liveness
+    mask, then bhg_encode_ikey_batch == the restated Writer.AddIkey sequence
+    (one destination table, source fileNums in the headers, given khash)."""
+    from oracle import table as T
+    from bitalosdb_amd.codec import as_device_bytes, _u64_tensor
+    rng = random.Random(30 + codec_kind)
+    st = T.Store(1 << 20, compressor=codec_kind)
+    s = st.flush_start()
+    for i in range(1500):
+        s.add(b"compact_key_%05d" % i, i + 1, compressible(rng, rng.choice([100, 900, 2000])))
+    s.compact = True
+    s.finish()
+    blobs = [bytes(st.files[fn]) for fn in sorted(st.files)]
+    src = b"".join(blobs)
+    toff = np.cumsum([0] + [len(b) for b in blobs]).astype(np.uint64)
+    h_t, first, _ = codec.scan_tables(as_device_bytes(src, codec.device), _u64_tensor(toff, codec.device), mode=0)
+    codec.sync()
+    h = h_t.cpu().numpy().view(O.HANDLE_DT).reshape(-1)
+    assert len(h) == 1500
+    desc, _, _ = codec.decode(src, h)          # stored bytes: NoCompressor view even for snappy tables
+    assert (desc["status"] == 0).all()
+    sb = np.frombuffer(src, np.uint8)
+    keys, vals, trs, fns = [], [], [], []
+    for i in range(len(h)):
+        o = int(h["offset"][i])
+        keys.append(sb[o + 12:o + 12 + int(desc["key_len"][i])].tobytes())
+        vals.append(sb[o + int(desc["val_off"][i]):o + int(desc["val_off"][i]) + int(desc["val_len"][i])].tobytes())
+        trs.append(int(desc["trailer"][i]))
+        fns.append(int(desc["file_num"][i]))
+    live = np.array([rng.random() < 0.7 for _ in keys], dtype=np.uint8)
+    init = 4096
+    got = codec.encode_ikey(keys, trs, vals, fns, live=live, khash=desc["fnv1"], init_size=init)
+    w = T.Writer(99, 1 << 40, compressor=codec_kind)
+    w.current_offset = w.size = init
+    w.file += bytes(init)
+    exp_bh = []
+    for i in range(len(keys)):
+        if live[i]:
+            exp_bh.append(w.add_ikey(keys[i], trs[i], vals[i], int(desc["fnv1"][i]), fns[i]))
+    assert (got["status"][live == 0] == O.SKIPPED).all() and (got["status"][live == 1] == 0).all()
+    assert int(got["summary"][2]) == 0
+    gbh = list(zip(got["bh_off"][live == 1].tolist(), got["bh_len"][live == 1].tolist()))
+    assert gbh == exp_bh
+    assert got["out"].tobytes() == bytes(w.file[init:w.current_offset])
+    assert (got["table"] == 0).all() and np.array_equal(got["fnv"], desc["fnv1"])
+    # the re-packed records decode with their source fileNums and CRCs
+    hh = np.zeros(int(live.sum()), dtype=O.HANDLE_DT)
+    hh["offset"] = got["pos"][live == 1]
+    hh["length"] = got["bh_len"][live == 1]
+    d2, _, _ = codec.decode(got["out"], hh)
+    assert (d2["status"] == 0).all()
+    assert np.array_equal(d2["file_num"], np.array(fns, np.uint32)[live == 1])
+    assert np.array_equal(d2["crc"], got["crc"][live == 1])
