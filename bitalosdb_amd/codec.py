@@ -296,6 +296,53 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_fnv32_batch")
         return out
 
+    def table_tail(self, recs_t, rec_t, bh_off_t, khash_t, table_t, status_t, n, ntables, data_end_t, tail_cap=None):
+        """bhg_table_tail: Writer.writeTable's tail for `ntables` tables on the GPU.
+        All inputs are device tensors (rec_t: bhg_handle[n] as int64 pairs).
+        tail_cap None sizes the buffer exactly (one sizing call first).
+        Returns (tail uint8 tensor, tail_off int64 [ntables+1], tail_len int64
+        [ntables], stats int32 [4*ntables])."""
+        dev = self.device
+        with torch.cuda.stream(self.stream):
+            off = torch.zeros(ntables + 1, dtype=torch.int64, device=dev)
+            ln = torch.zeros(max(ntables, 1), dtype=torch.int64, device=dev)
+            stats = torch.zeros(max(ntables, 1) * 4, dtype=torch.int32, device=dev)
+        args = lambda tail, cap: (self.ctx, _ptr(recs_t), _ptr(rec_t), _ptr(bh_off_t), _ptr(khash_t), _ptr(table_t),
+                                  _ptr(status_t), n, ntables, _ptr(data_end_t), _ptr(tail), cap, _ptr(off), _ptr(ln),
+                                  _ptr(stats), self._stream())
+        if tail_cap is None:
+            B.check(self.ctx, self.L.bhg_table_tail(*args(None, 0)), "bhg_table_tail(sizing)")
+            self.sync()
+            tail_cap = int(off[ntables].item())
+        with torch.cuda.stream(self.stream):
+            tail = torch.zeros(max(tail_cap, 1), dtype=torch.uint8, device=dev)
+        B.check(self.ctx, self.L.bhg_table_tail(*args(tail, tail_cap)), "bhg_table_tail")
+        return tail, off, ln[:ntables], stats[:4 * ntables]
+
+    def rebuild_tables(self, src_t, table_off):
+        """bhg_rebuild_tables (Writer.rebuild, writer.go:539-583) over footerless
+        tables src_t[table_off[t]:table_off[t+1]].  Returns device tensors
+        (handles int64 pairs [count], first [ntables+1], end [ntables],
+        khash/bh_off/table int32 [count])."""
+        ntab = len(table_off) - 1
+        dev = self.device
+        with torch.cuda.stream(self.stream):
+            toff = table_off if torch.is_tensor(table_off) else _u64_tensor(table_off, dev)
+            first = torch.zeros(ntab + 1, dtype=torch.int64, device=dev)
+            end = torch.zeros(max(ntab, 1), dtype=torch.int64, device=dev)
+        rc = self.L.bhg_scan_tables(self.ctx, _ptr(src_t), _ptr(toff), ntab, 1, None, 0, _ptr(first), _ptr(end),
+                                    self._stream())
+        B.check(self.ctx, rc, "bhg_scan_tables(count)")
+        self.sync()
+        cnt = int(first[ntab].item())
+        with torch.cuda.stream(self.stream):
+            h = torch.empty((max(cnt, 1), 2), dtype=torch.int64, device=dev)
+            kh, bo, tb = (torch.empty(max(cnt, 1), dtype=torch.int32, device=dev) for _ in range(3))
+        rc = self.L.bhg_rebuild_tables(self.ctx, _ptr(src_t), _ptr(toff), ntab, _ptr(h), cnt, _ptr(first), _ptr(end),
+                                       _ptr(kh), _ptr(bo), _ptr(tb), self._stream())
+        B.check(self.ctx, rc, "bhg_rebuild_tables")
+        return h[:cnt], first, end[:ntab], kh[:cnt], bo[:cnt], tb[:cnt]
+
     def scan_tables(self, src_t, table_off, mode=0, max_out=None):
         """TableIterator (mode 0, table.go:358-395) / Writer.rebuild (mode 1,
         writer.go:539-583) header chase over each table src_t[table_off[t]:table_off[t+1]].
@@ -352,6 +399,8 @@ class EncodeBuffers:
         self.status = z(n, torch.int32)
         self.table_start = z(max_tables, torch.int32)
         self.summary = z(4, torch.int64)
+        self.rec = z(max(n, 1) * 2, torch.int64)           # bhg_handle[n]
+        self.table_size = z(max_tables, torch.int64)
 
     def struct(self):
         return B.EncodeOut(*[_ptr(getattr(self, f)) for f, _ in B.EncodeOut._fields_])
@@ -392,7 +441,7 @@ def _encode_result(bufs, out, nt):
     return dict(out=out[:min(total, out.numel())].cpu().numpy(), pos=bufs.pos.cpu().numpy().view(np.uint64),
                 bh_off=u32(bufs.bh_off), bh_len=u32(bufs.bh_len), table=u32(bufs.table), fnv=u32(bufs.fnv1),
                 crc=u32(bufs.crc), status=u32(bufs.status), table_start=u32(bufs.table_start)[:nt], ntables=nt,
-                summary=summ.copy())
+                summary=summ.copy(), bufs=bufs, out_t=out)
 
 
 def _encode(self, keys, trailers, values, compressor=NoCompressor, file_nums=(1,), init_size=0,
@@ -451,3 +500,37 @@ BithashCodec.encode_batch = _encode_codec
 BithashCodec.encode_ikey_batch = _encode_ikey_codec
 BithashCodec.encode = _encode
 BithashCodec.encode_ikey = _encode_ikey
+
+
+def _encode_tables(self, keys, trailers, values, compressor=NoCompressor, file_nums=(1,), table_max=128 << 20):
+    """A whole flush on the GPU: BithashWriter.Add over the batch (table
+    splits included), then every table closed with Writer.writeTable
+    (bhg_table_tail).  Returns {fileNum: table file bytes} plus the encode
+    result; the mirror of FlushStart/Add.../FlushFinish on a compacting flush
+    (bithash_writer.go:25-87) where every table is finished."""
+    res = self.encode(keys, trailers, values, compressor=compressor, file_nums=file_nums, table_max=table_max)
+    dev = self.device
+    nt = res["ntables"]
+    bufs = res["bufs"]
+    with torch.cuda.stream(self.stream):
+        out_t = res["out_t"]
+        tail, off, ln, stats = self.table_tail(out_t, bufs.rec, bufs.bh_off, bufs.fnv1, bufs.table, bufs.status,
+                                               len(keys), nt, bufs.table_size)
+        self.sync()
+    tail = tail.cpu().numpy()
+    off = off.cpu().numpy()
+    ln = ln.cpu().numpy()
+    sizes = bufs.table_size.cpu().numpy()[:nt]
+    out = res["out"]
+    files = {}
+    ts = list(res["table_start"]) + [len(keys)]
+    pos = res["pos"]
+    for t in range(nt):
+        ok = [i for i in range(ts[t], ts[t + 1]) if res["status"][i] == 0]
+        start = int(pos[ok[0]]) - int(res["bh_off"][ok[0]]) if ok else 0
+        data = out[start:start + int(sizes[t])].tobytes() if ok else b""
+        files[int(file_nums[t])] = data + tail[int(off[t]):int(off[t]) + int(ln[t])].tobytes()
+    return files, res, stats.cpu().numpy().view(np.uint32).reshape(-1, 4)
+
+
+BithashCodec.encode_tables = _encode_tables

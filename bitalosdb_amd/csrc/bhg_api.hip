@@ -608,4 +608,38 @@ int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, u
     return BHG_OK;
 }
 
+int bhg_table_tail(bhg_ctx *c, const uint8_t *recs, const bhg_handle *rec, const uint32_t *bh_off,
+                   const uint32_t *khash, const uint32_t *table, const uint32_t *status, uint32_t n,
+                   uint32_t ntables, const uint64_t *data_end, uint8_t *tail, uint64_t tail_cap,
+                   uint64_t *tail_off, uint64_t *tail_len, uint32_t *stats, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (!tail_off) { set_err(c, "table tail needs tail_off[ntables+1]"); return BHG_EINVAL; }
+    if (ntables == 0) return bhg_memset_device(c, tail_off, 0, 8, stream);
+    if (!data_end || !tail_len || (!tail && tail_cap)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (n && (!recs || !rec || !bh_off || !khash || !table)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    Scratch sc;
+    if (int r = scratch_alloc(c, L.stream, bhg::tail_scratch_bytes(n, ntables), sc)) return r;
+    bhg::TailLaunch T;
+    T.recs = recs; T.rec = rec; T.bh_off = bh_off; T.khash = khash; T.table = table; T.status = status;
+    T.n = n; T.ntables = ntables; T.data_end = data_end; T.tail = tail; T.tail_cap = tail ? tail_cap : 0;
+    T.tail_off = tail_off; T.tail_len = tail_len; T.stats = stats;
+    HIP_TRY(c, bhg::launch_table_tail(L, T, sc.base));
+    return BHG_OK;
+}
+
+int bhg_rebuild_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables,
+                       bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
+                       uint32_t *out_khash, uint32_t *out_bh_off, uint32_t *out_table, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (max_out && (!out_khash || !out_bh_off || !out_table)) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    if (int r = bhg_scan_tables(c, src, table_off, ntables, 1, out_handles, max_out, out_first, out_end, stream))
+        return r;
+    if (ntables == 0 || max_out == 0) return BHG_OK;
+    HIP_TRY(c, bhg::launch_rebuild_recs(launch_of(c, stream), src, table_off, ntables, out_handles, max_out,
+                                        out_first, out_khash, out_bh_off, out_table));
+    return BHG_OK;
+}
+
 }  // extern "C"

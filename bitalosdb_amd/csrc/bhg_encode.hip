@@ -238,18 +238,41 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
             a.o.bh_off[i] = 0;
             a.o.bh_len[i] = 0;
             a.o.crc[i] = 0;
+            if (a.o.rec) a.o.rec[i] = bhg_handle{~0ull, 0, 0};
             continue;
         }
         a.o.pos[i] = P;
         const uint64_t P0 = a.lens[a.o.table_start[t]];
         a.o.bh_off[i] = (uint32_t)((t == 0 ? (uint64_t)a.init_size : 0ull) + (P - P0));
         a.o.bh_len[i] = L;
+        if (a.o.rec) a.o.rec[i] = bhg_handle{P, L, 0};
         a.o.crc[i] = crc_mask(~crc_range_a<8>(crc, 0xffffffffu, (uint64_t)a.out + P, L, out_end));
     }
     // summary[2]: failed adds (every status but OK / SKIPPED); one vector atomic per wave
     for (int d = 32; d >= 1; d >>= 1) failed += __shfl_xor(failed, d);
     if ((threadIdx.x & 63) == 0 && failed) atomicAdd(reinterpret_cast<unsigned long long *>(a.o.summary + 2),
                                                      (unsigned long long)failed);
+}
+
+// table_size[t]: the writer's currentOffset after the batch -- end of the
+// table's last successful add (init_size / 0 for a table with none)
+__global__ __launch_bounds__(256) void k_enc_tsize(EncArgs a) {
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.max_tables; t += gridDim.x * blockDim.x) {
+        uint64_t size = t == 0 ? a.init_size : 0;
+        if (t < ntab) {
+            const uint32_t s = a.o.table_start[t], e = t + 1 < ntab ? a.o.table_start[t + 1] : a.n;
+            for (uint32_t i = e; i > s; i--) {
+                if (a.o.status[i - 1] == BHG_ST_OK) {
+                    size = (uint64_t)a.o.bh_off[i - 1] + a.o.bh_len[i - 1];
+                    break;
+                }
+            }
+        } else {
+            size = 0;
+        }
+        a.o.table_size[t] = size;
+    }
 }
 
 // value' = raw values: vpos = val_off, vlen = val_off[i+1]-val_off[i]
@@ -280,6 +303,8 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     if (gc > capc) gc = capc;
     if (gc == 0) gc = 1;
     hipLaunchKernelGGL(k_enc_crc<16>, dim3(gc), dim3(512), 0, L.stream, a);
+    if (E.o.table_size)
+        hipLaunchKernelGGL(k_enc_tsize, dim3(lane_grid(L, E.max_tables, 256)), dim3(256), 0, L.stream, a);
     return hipGetLastError();
 }
 

@@ -87,6 +87,25 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
                              uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
                              uint16_t *gtables);
 
+// bhg_tail.hip: Writer.writeTable's tail for many tables (include/bithashgpu.h bhg_table_tail)
+struct TailLaunch {
+    const uint8_t *recs;
+    const bhg_handle *rec;
+    const uint32_t *bh_off, *khash, *table, *status;
+    uint32_t n, ntables;
+    const uint64_t *data_end;
+    uint8_t *tail;
+    uint64_t tail_cap;
+    uint64_t *tail_off, *tail_len;
+    uint32_t *stats;
+};
+size_t tail_scratch_bytes(uint32_t n, uint32_t ntables);
+hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch);
+// bhg_tscan.hip: per-record rebuild outputs after a mode-1 scan (khash, table-relative offset, table)
+hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables,
+                               const bhg_handle *h, uint64_t max_out, const uint64_t *first, uint32_t *khash,
+                               uint32_t *bh_off, uint32_t *table);
+
 // bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
 // scratch must hold scan_scratch_bytes(n).
 size_t scan_scratch_bytes(uint64_t n);

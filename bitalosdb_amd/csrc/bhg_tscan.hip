@@ -160,7 +160,46 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
     }
 }
 
+// Writer.rebuild's per-record work after the header chase (writer.go:569-575):
+// bh = {offset inside the table, recordLen}, khash = hash.Fnv32(UserKey) of
+// base.DecodeInternalKey(key) (UserKey empty when ikeySize < 8), table index.
+// Entries past the scanned count get table = UINT32_MAX.
+__global__ __launch_bounds__(256) void k_rebuild_recs(const uint8_t *src, const uint64_t *table_off, uint32_t ntables,
+                                                      const bhg_handle *h, uint64_t max_out, const uint64_t *first,
+                                                      uint32_t *khash, uint32_t *bh_off, uint32_t *table) {
+    const uint64_t total = first[ntables];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < max_out;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i >= total) {
+            table[i] = 0xffffffffu;
+            khash[i] = 0;
+            bh_off[i] = 0;
+            continue;
+        }
+        uint32_t lo = 0, hi = ntables;  // last t with first[t] <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (first[mid] <= i) lo = mid; else hi = mid;
+        }
+        const bhg_handle r = h[i];
+        const uint64_t p = (uint64_t)src + r.offset, tend = (uint64_t)src + table_off[lo + 1];
+        const uint32_t k = ldu32(p, tend);  // the chase read this header and its key inside the table
+        table[i] = lo;
+        bh_off[i] = (uint32_t)(r.offset - table_off[lo]);
+        khash[i] = fnv1_range(p + 12, k >= 8 ? k - 8 : 0, tend);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables,
+                               const bhg_handle *h, uint64_t max_out, const uint64_t *first, uint32_t *khash,
+                               uint32_t *bh_off, uint32_t *table) {
+    if (max_out == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rebuild_recs, dim3(lane_grid(L, max_out, 256)), dim3(256), 0, L.stream, src, table_off,
+                       ntables, h, max_out, first, khash, bh_off, table);
+    return hipGetLastError();
+}
 
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                         bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch) {

@@ -222,6 +222,10 @@ typedef struct bhg_encode_out {
     uint64_t *summary;      /* [4]: bytes the batch occupies in out (out_cap >= this
                                writes every record), tables used (0 = max_tables too
                                small), failed adds (status not OK/SKIPPED), split failed */
+    bhg_handle *rec;        /* nullable: {pos, bh_len} per record ({UINT64_MAX, 0} if not written):
+                               the record list bhg_table_tail / bhg_decode_batch take */
+    uint64_t *table_size;   /* nullable [max_tables]: currentOffset of each table after the
+                               batch (its data-region size; bhg_table_tail's data_end) */
 } bhg_encode_out;
 
 int bhg_encode_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
@@ -250,6 +254,48 @@ int bhg_encode_ikey_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key
                           const uint8_t *vals, const uint64_t *val_off, uint32_t n, const uint32_t *khash,
                           const uint32_t *rec_file_nums, const uint8_t *live, uint32_t init_size, uint8_t *out,
                           uint64_t out_cap, const bhg_encode_out *o, void *stream);
+
+/* ---- table tail (device): Writer.writeTable for many tables at once ----
+ * Replaces writeData's empty record header, writeConflict, writeIndexHash,
+ * writeMeta and writeFooter (bithash/writer.go:312-338, 393-533), with
+ * updateHash (writer.go:285-310) folded over the records in add order, the
+ * HashIndex build/serialize (internal/bindex/hash_index.go:217-363), the
+ * blockWriter format (block.go:595-729) and the footer (table.go:56-68).
+ *   recs, rec[n]     : record bytes and each record's {position in recs, length}
+ *                      (bhg_encode_out.rec, or bhg_rebuild_tables' handles)
+ *   bh_off[n]        : BlockHandle.Offset of each record inside its table
+ *   khash[n]         : the khash updateHash was given (hash.Fnv32(userKey) for Add)
+ *   table[n]         : table index; records with table >= ntables are ignored
+ *   status[n]        : nullable; records with status != BHG_ST_OK are ignored
+ *   data_end[ntables]: each table's currentOffset before writeTable (its data size)
+ *   tail, tail_cap   : output; table t's tail bytes are written at tail + tail_off[t]
+ *   tail_off[ntables+1] : written: slot offsets (exclusive scan of per-table upper
+ *                      bounds); tail_off[ntables] = bytes needed
+ *   tail_len[ntables]: written: bytes of table t's tail (the file is its data region
+ *                      followed by these bytes); 0 when its slot ends past tail_cap
+ *   stats[4*ntables] : nullable; per table {index items, conflict keys, BHG_ST_OK or
+ *                      BHG_ST_NO_SPACE, 0}
+ * Records of one table must be given in add order (the order Add was called).
+ * Asynchronous on `stream`. */
+int bhg_table_tail(bhg_ctx *ctx, const uint8_t *recs, const bhg_handle *rec, const uint32_t *bh_off,
+                   const uint32_t *khash, const uint32_t *table, const uint32_t *status, uint32_t n,
+                   uint32_t ntables, const uint64_t *data_end, uint8_t *tail, uint64_t tail_cap,
+                   uint64_t *tail_off, uint64_t *tail_len, uint32_t *stats, void *stream);
+
+/* ---- rebuild (device): Writer.rebuild over footerless tables ----
+ * Replaces writer.go:539-583 (and the reopen path that calls it): the mode-1
+ * header chase of bhg_scan_tables, then per record bh = {offset inside the
+ * table, 12 + ikeySize + valueSize}, khash = hash.Fnv32(UserKey) and the
+ * table index -- exactly the inputs updateHash received, so bhg_table_tail
+ * on them (with data_end = out_end) writes the tail Writer.writeTable would
+ * write after the rebuild.
+ *   src, table_off, ntables, out_handles, max_out, out_first, out_end : as
+ *       bhg_scan_tables mode 1 (out_end[t] = the rebuilt currentOffset)
+ *   out_khash, out_bh_off, out_table [max_out] : per record; entries past
+ *       out_first[ntables] get table = UINT32_MAX */
+int bhg_rebuild_tables(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_off, uint32_t ntables,
+                       bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
+                       uint32_t *out_khash, uint32_t *out_bh_off, uint32_t *out_table, void *stream);
 
 /* ---- table data-region scan (device) ----
  * TableIterator.findEntry (bithash/table.go:358-395, mode 0) or Writer.rebuild
