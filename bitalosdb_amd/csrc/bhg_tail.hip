@@ -29,6 +29,7 @@
 //   k_conf_write   lane/rank: the entry bytes, restart array, count
 //   k_tail_items   lane/run: the 10-byte big-endian HashIndex item
 //   k_tail_shards  lane/(table, shard): cumulative shard count (big-endian)
+//   k_tail_crch    lane/table: HashIndex header, checksum range
 //   k_crc_long     the indexhash_data checksum (bhg_decode.hip)
 //   k_tail_finish  lane/table: block headers, checksum entry, meta block, footer
 #include <rocprim/device/device_radix_sort.hpp>
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(256) void k_tail_shards(TailArgs a) {
         const uint32_t t = (uint32_t)(x / kShards), s = (uint32_t)(x % kShards);
         const uint32_t r0 = a.tab_run[t], r1 = a.tab_run[t + 1];
         if (r0 == r1 || !tail_fits(a, t)) continue;
-        const uint64_t lim = (uint64_t)t << 32 | (uint64_t)(s + 1) << 16;  // first key past shard s
+        const uint64_t lim = ((uint64_t)t << 32) + ((uint64_t)(s + 1) << 16);  // first key past shard s (s = 65535: next table)
         const uint32_t cnt = lower_bound(r0, r1, lim, [&](uint32_t r) { return a.run_key[r]; }) - r0;
         uint64_t dpos, dlen;
         idx_data(a, t, r1 - r0, dpos, dlen);
@@ -379,7 +380,13 @@ __global__ __launch_bounds__(256) void k_tail_crch(TailArgs a) {
         h.offset = dpos;
         h.length = (uint32_t)dlen;
         h.pad = 0;
-        if (!tail_fits(a, (uint32_t)t)) h.offset = ~0ull;  // out of range -> not computed
+        if (!tail_fits(a, (uint32_t)t)) {
+            h.offset = ~0ull;  // out of range -> not computed
+        } else if (Rt) {       // HashIndex header (big-endian): version 1, reserved 0, shards 65536
+            const uint64_t p = (uint64_t)a.tail + dpos;
+            st8(p, 0); st8(p + 1, 1); st8(p + 2, 0); st8(p + 3, 0);
+            st8(p + 4, 0); st8(p + 5, 1); st8(p + 6, 0); st8(p + 7, 0);
+        }
         a.crc_h[t] = h;
     }
 }
@@ -413,10 +420,7 @@ __global__ __launch_bounds__(64) void k_tail_finish(TailArgs a) {
             p = put_varint(p, dlen);
             p = put_str(p, "indexhash_data", 14);
             p = put_trailer(p);
-            // HashIndex header (big-endian): version 1, reserved 0, shards 65536
-            st8(p, 0); st8(p + 1, 1); st8(p + 2, 0); st8(p + 3, 0);
-            st8(p + 4, 0); st8(p + 5, 1); st8(p + 6, 0); st8(p + 7, 0);
-            p += dlen;
+            p += dlen;  // header (k_tail_crch), shards, items: written before the checksum
         }
         // indexhash_checksum: strconv.FormatUint(crc.New(data).Value(), 10)
         char dig[10];

@@ -137,7 +137,7 @@ def test_tail_small_cap_reports_no_space(codec):
     keys = [rb(rng, 12) for _ in range(500)]
     vals = [rb(rng, 100) for _ in range(500)]
     trs = [((i + 1) << 8) | 1 for i in range(500)]
-    res = codec.encode(keys, trs, vals, file_nums=[1, 2, 3], table_max=20000)
+    res = codec.encode(keys, trs, vals, file_nums=list(range(1, 20)), table_max=20000)
     nt = res["ntables"]
     bufs = res["bufs"]
     _, off_full, ln_full, _ = codec.table_tail(res["out_t"], bufs.rec, bufs.bh_off, bufs.fnv1, bufs.table,
