@@ -35,6 +35,7 @@ EXPORTS = [
     "bhg_memcpy_h2d", "bhg_memcpy_d2h", "bhg_memset_device", "bhg_decode_batch", "bhg_decode_batch_host",
     "bhg_crc32c_masked_batch", "bhg_crc32c_masked_long", "bhg_fnv32_batch", "bhg_encode_batch",
     "bhg_encode_ikey_batch", "bhg_scan_tables", "bhg_table_tail", "bhg_rebuild_tables",
+    "bhg_repack_batch",
     "bhg_host_register", "bhg_host_unregister", "bhg_get_batch",
 ]
 
@@ -95,6 +96,7 @@ def lib():
             "bhg_scan_tables": (I, [P, P, P, U32, I, P, U64, P, P, P]),
             "bhg_table_tail": (I, [P, P, P, P, P, P, P, U32, U32, P, P, U64, P, P, P, P]),
             "bhg_rebuild_tables": (I, [P, P, P, U32, P, U64, P, P, P, P, P, P]),
+            "bhg_repack_batch": (I, [P, P, U64, P, U32, P, P, U32, P, U64, ctypes.POINTER(EncodeOut), P]),
             "bhg_host_register": (I, [P, P, U64]),
             "bhg_host_unregister": (I, [P, P]),
             "bhg_get_batch": (I, [P, P, U64, P, U32, P, P, P, P, U32, P, P, P]),

@@ -534,3 +534,49 @@ def _encode_tables(self, keys, trailers, values, compressor=NoCompressor, file_n
 
 
 BithashCodec.encode_tables = _encode_tables
+
+
+def _repack_batch(self, src_t, handles_t, n, live_t=None, khash_t=None, init_size=0, out_t=None, bufs=None):
+    """bhg_repack_batch: the live records of a TableIterator pass re-packed
+    byte for byte into one destination table (compaction's AddIkey loop)."""
+    dev = self.device
+    with torch.cuda.stream(self.stream):
+        if out_t is None:
+            out_t = torch.zeros(max(src_t.numel(), 1), dtype=torch.uint8, device=dev)
+        if bufs is None:
+            bufs = EncodeBuffers(n, 1, dev)
+    o = bufs.struct()
+    rc = self.L.bhg_repack_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(handles_t), n, _ptr(live_t),
+                                 _ptr(khash_t), init_size, _ptr(out_t), out_t.numel(), ctypes.byref(o), self._stream())
+    B.check(self.ctx, rc, "bhg_repack_batch")
+    return out_t, bufs
+
+
+def _compact(self, src_t, table_off, live=None, init_size=0):
+    """compactBithashFiles (bitree/bithash.go:158-270) for the bithash side, all
+    on the GPU: TableIterator scan of every source table (bhg_scan_tables mode
+    0), the liveness filter + AddIkey re-pack (bhg_repack_batch), and the
+    destination's Writer.writeTable (bhg_table_tail).  live: per scanned record
+    (scan order), host or device u8; None keeps everything.
+    Returns (table file bytes, per-record statuses, handles numpy)."""
+    dev = self.device
+    h_t, first, _ = self.scan_tables(src_t, table_off, mode=0)
+    self.sync()
+    n = int(h_t.shape[0]) if int(first[-1].item()) else 0
+    with torch.cuda.stream(self.stream):
+        live_t = None
+        if live is not None:
+            live_t = live if torch.is_tensor(live) else torch.from_numpy(np.ascontiguousarray(live, np.uint8)).to(dev)
+    out_t, bufs = self.repack_batch(src_t, h_t, n, live_t, None, init_size)
+    tail, off, ln, stats = self.table_tail(out_t, bufs.rec, bufs.bh_off, bufs.fnv1, bufs.table, bufs.status, n, 1,
+                                           bufs.table_size)
+    self.sync()
+    size = int(bufs.table_size[0].item())
+    data = out_t[:size - init_size].cpu().numpy().tobytes()
+    t = tail.cpu().numpy()
+    return data + t[int(off[0]):int(off[0]) + int(ln[0])].tobytes(), bufs.status.cpu().numpy().view(np.uint32)[:n], \
+        h_t.cpu().numpy().view(HANDLE_DT).reshape(-1)[:n]
+
+
+BithashCodec.repack_batch = _repack_batch
+BithashCodec.compact = _compact

@@ -593,6 +593,39 @@ int bhg_encode_ikey_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_o
     return BHG_OK;
 }
 
+int bhg_repack_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                     const uint8_t *live, const uint32_t *khash, uint32_t init_size, uint8_t *out, uint64_t out_cap,
+                     const bhg_encode_out *o, void *stream) {
+    if (!c) return BHG_EINVAL;
+    if (!encode_outputs_ok(c, o, n, 1)) return BHG_EINVAL;
+    if (int r = set_device(c)) return r;
+    bhg::Launch L = launch_of(c, stream);
+    if (n == 0) return encode_empty(c, o, L.stream);
+    if (!src || !handles || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
+    const size_t N = (size_t)n + 1;
+    Scratch sc;
+    if (int r = scratch_alloc(c, L.stream, 7 * N * 8 + 3 * N * 4 + bhg::scan_scratch_bytes(n) + 12 * 256, sc)) return r;
+    bhg::EncodeLaunch E;
+    memset(&E, 0, sizeof E);
+    E.lens = reinterpret_cast<uint64_t *>(sc.take(N * 8));
+    E.scan_scratch = sc.take(bhg::scan_scratch_bytes(n));
+    uint64_t *key_off = reinterpret_cast<uint64_t *>(sc.take(N * 8));
+    uint32_t *key_len = reinterpret_cast<uint32_t *>(sc.take(N * 4));
+    uint64_t *trailers = reinterpret_cast<uint64_t *>(sc.take(N * 8));
+    uint64_t *vpos = reinterpret_cast<uint64_t *>(sc.take(N * 8));
+    uint64_t *vlen = reinterpret_cast<uint64_t *>(sc.take(N * 8));
+    uint32_t *fns = reinterpret_cast<uint32_t *>(sc.take(N * 4));
+    uint32_t *pre = reinterpret_cast<uint32_t *>(sc.take(N * 4));
+    HIP_TRY(c, bhg::launch_repack_prep(L, src, src_len, handles, n, key_off, key_len, trailers, vpos, vlen, fns, pre));
+    E.keys = src; E.key_off = key_off; E.key_len = key_len; E.trailers = trailers;
+    E.vbase = src; E.vpos = vpos; E.vlen = vlen; E.n = n;
+    E.file_nums = fns; E.rec_file_nums = fns; E.live = live; E.khash = khash; E.pre_status = pre;
+    E.single_table = 1; E.max_tables = 1; E.init_size = init_size; E.table_max = UINT64_MAX;
+    E.out = out; E.out_cap = out_cap; E.o = *o;
+    HIP_TRY(c, bhg::launch_encode(L, E));
+    return BHG_OK;
+}
+
 int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                     bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end, void *stream) {
     if (!c) return BHG_EINVAL;

@@ -34,6 +34,8 @@ struct EncArgs {
     const uint32_t *rec_file_nums;  // AddIkey: header fileNum per record (nullable -> file_nums[table])
     const uint8_t *live;          // compaction liveness mask (nullable -> all live)
     const uint32_t *khash;        // AddIkey: given khash per record (nullable -> FNV-1 of the key)
+    const uint32_t *key_len;      // nullable: key i = keys[key_off[i] .. + key_len[i]) (else key_off[i+1] ends it)
+    const uint32_t *pre_status;   // nullable: non-OK -> the record is not added (repack's record checks)
     int single_table;             // AddIkey: one table, no split, dataMaxSize checked per record
     uint32_t max_tables;
     uint32_t init_size;
@@ -43,6 +45,10 @@ struct EncArgs {
     uint64_t *lens;               // scratch: L per record, then exclusive scan -> positions (n+1)
     bhg_encode_out o;
 };
+
+__device__ __forceinline__ uint32_t key_len_of(const EncArgs &a, uint32_t i) {
+    return a.key_len != nullptr ? a.key_len[i] : (uint32_t)(a.key_off[i + 1] - a.key_off[i]);
+}
 
 #define BHG_DATA_MAX_SIZE (0xFFFFFFFFull - (256ull << 20))  // writer.go:45
 
@@ -58,11 +64,12 @@ __device__ __forceinline__ uint32_t fit_status(const EncArgs &a, uint64_t P, uin
 
 __global__ __launch_bounds__(256) void k_enc_sizes(EncArgs a) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-        const uint64_t klen = a.key_off[i + 1] - a.key_off[i];
+        const uint64_t klen = key_len_of(a, i);
         const uint64_t vl = a.vlen[i];
         uint32_t st = BHG_ST_OK;
         uint64_t L = 0;
         if (a.live != nullptr && a.live[i] == 0) st = BHG_ST_SKIPPED;           // bitree/bithash.go:225-228
+        else if (a.pre_status != nullptr && a.pre_status[i] != BHG_ST_OK) st = a.pre_status[i];
         else if (klen + 8 > BHG_MAX_KEY_SIZE) st = BHG_ST_KEY_TOO_LARGE;
         else if (vl == ~0ull) st = BHG_ST_NO_SPACE;                              // snappy scratch overflow
         else if (vl > BHG_MAX_VALUE_SIZE) st = BHG_ST_VALUE_TOO_LARGE;
@@ -153,13 +160,12 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
     const uint32_t nw = gridDim.x * ENC_WAVES;
     const uint32_t ntab = (uint32_t)a.o.summary[1];
     if (ntab == 0) return;  // split failed (max_tables too small)
-    const uint64_t vend = ~0ull;
     for (uint32_t r = blockIdx.x * ENC_WAVES + (threadIdx.x >> 6); r < a.n; r += nw) {
         if (a.o.status[r] != BHG_ST_OK) continue;
         const uint64_t P = a.lens[r];
         const uint32_t L = (uint32_t)(a.lens[r + 1] - P);
         if (fit_status(a, P, L) != BHG_ST_OK) continue;
-        const uint32_t klen = (uint32_t)(a.key_off[r + 1] - a.key_off[r]);
+        const uint32_t klen = key_len_of(a, r);
         const uint32_t vl = (uint32_t)a.vlen[r];
         const uint32_t t = table_of(a.o.table_start, ntab, r);
         const uint32_t fn = a.rec_file_nums != nullptr ? a.rec_file_nums[r] : a.file_nums[t];
@@ -177,11 +183,12 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                 // whole dword inside the value: unaligned source read (2 aligned loads + alignbyte)
                 const uint64_t s = vp + (uint64_t)(o0 - pre);
                 const uint64_t sa = s & ~3ull;
+                // an aligned dword holding a byte of the value is mapped; the one after it may
+                // not be (the value can end the caller's buffer at a page boundary)
                 const uint32_t lo = gld<uint32_t>(sa);
                 const uint32_t sh = (uint32_t)(s & 3);
-                const uint32_t hi = sh ? gld<uint32_t>(sa + 4) : 0u;
+                const uint32_t hi = sh && sa + 4 < vp + vl ? gld<uint32_t>(sa + 4) : 0u;
                 w = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-                (void)vend;
                 if (o0 + 4 <= (int64_t)L) {
                     gst<uint32_t>(q, w);
                     continue;
@@ -222,7 +229,7 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
     uint32_t failed = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
         const uint64_t kp = (uint64_t)a.keys + a.key_off[i];
-        const uint32_t klen = (uint32_t)(a.key_off[i + 1] - a.key_off[i]);
+        const uint32_t klen = key_len_of(a, i);
         // writer.go:246 (Add: FNV-1 of every key, before add()) / :249 (AddIkey: the caller's khash)
         a.o.fnv1[i] = a.khash != nullptr ? a.khash[i] : fnv1_range(kp, klen, kp + klen);
         const uint32_t t = ntab ? table_of(a.o.table_start, ntab, i) : 0;
@@ -281,11 +288,57 @@ __global__ __launch_bounds__(256) void k_enc_rawvals(const uint64_t *val_off, ui
         vlen[i] = val_off[i + 1] - val_off[i];
 }
 
+// Compaction re-pack from stored records (bhg_repack_batch): the AddIkey
+// inputs of each record read straight from its bytes -- what TableIterator
+// hands compactBithashFiles (table.go:358-395: ikey, stored value, header
+// fileNum).  A handle that is out of range or not a whole record
+// (12 + ikeySize + valueSize != length, ikeySize < 8) -> RECORD_NIL.
+__global__ __launch_bounds__(256) void k_repack_prep(const uint8_t *src, uint64_t src_len, const bhg_handle *h,
+                                                     uint32_t n, uint64_t *key_off, uint32_t *key_len,
+                                                     uint64_t *trailers, uint64_t *vpos, uint64_t *vlen,
+                                                     uint32_t *fns, uint32_t *pre) {
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const bhg_handle r = h[i];
+        uint32_t st = BHG_ST_RECORD_NIL, k = 8, v = 0, fn = 0;
+        uint64_t tr = 0;
+        if (r.length >= 20 && r.offset <= src_len && (uint64_t)r.length <= src_len - r.offset) {
+            const uint64_t p = base + r.offset;
+            k = ldu32(p, end);
+            v = ldu32(p + 4, end);
+            fn = ldu32(p + 8, end);
+            if (k >= 8 && 12ull + k + v == r.length) {
+                st = BHG_ST_OK;
+                tr = ldu64(p + 12 + k - 8, end);
+            } else {
+                k = 8;
+                v = 0;
+            }
+        }
+        key_off[i] = r.offset + 12;
+        key_len[i] = k - 8;
+        trailers[i] = tr;
+        vpos[i] = r.offset + 12 + k;
+        vlen[i] = v;
+        fns[i] = fn;
+        pre[i] = st;
+    }
+}
+
+hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                              uint64_t *key_off, uint32_t *key_len, uint64_t *trailers, uint64_t *vpos,
+                              uint64_t *vlen, uint32_t *fns, uint32_t *pre) {
+    hipLaunchKernelGGL(k_repack_prep, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, src, src_len, h, n, key_off,
+                       key_len, trailers, vpos, vlen, fns, pre);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     EncArgs a;
     a.keys = E.keys; a.key_off = E.key_off; a.trailers = E.trailers;
     a.vals = E.vbase; a.vpos = E.vpos; a.vlen = E.vlen;
     a.n = E.n; a.file_nums = E.file_nums; a.rec_file_nums = E.rec_file_nums; a.live = E.live; a.khash = E.khash;
+    a.key_len = E.key_len; a.pre_status = E.pre_status;
     a.single_table = E.single_table; a.max_tables = E.max_tables; a.init_size = E.init_size;
     a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
     const uint32_t g = lane_grid(L, E.n, 256);

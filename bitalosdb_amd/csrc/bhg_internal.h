@@ -66,6 +66,8 @@ struct EncodeLaunch {
     const uint32_t *rec_file_nums;  // per record (AddIkey), nullable
     const uint8_t *live;            // per record liveness (compaction), nullable
     const uint32_t *khash;          // per record given khash (AddIkey), nullable -> FNV-1 of the key
+    const uint32_t *key_len;        // nullable: per-record key length (keys not contiguous)
+    const uint32_t *pre_status;     // nullable: records with a non-OK status here are not added
     int single_table;               // AddIkey: one table, no split; dataMaxSize checked per record
     uint32_t max_tables;
     uint32_t init_size;
@@ -78,6 +80,10 @@ struct EncodeLaunch {
 };
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E);
 hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen);
+// bhg_repack_batch: AddIkey inputs parsed from stored records
+hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                              uint64_t *key_off, uint32_t *key_len, uint64_t *trailers, uint64_t *vpos,
+                              uint64_t *vlen, uint32_t *fns, uint32_t *pre);
 
 // bhg_snappy_enc.hip
 hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *out);

@@ -255,6 +255,23 @@ int bhg_encode_ikey_batch(bhg_ctx *ctx, const uint8_t *keys, const uint64_t *key
                           const uint32_t *rec_file_nums, const uint8_t *live, uint32_t init_size, uint8_t *out,
                           uint64_t out_cap, const bhg_encode_out *o, void *stream);
 
+/* ---- compaction re-pack from stored records (device) ----
+ * bhg_encode_ikey_batch with the AddIkey inputs read straight from the
+ * source records: TableIterator hands compactBithashFiles each record's
+ * ikey, stored value bytes and header fileNum (table.go:358-395), and
+ * AddIkey writes them unchanged (writer.go:249-255), so the live records are
+ * re-packed byte for byte into one destination table.
+ *   src, src_len, handles[n] : source records (e.g. bhg_scan_tables mode 0
+ *                              over the tables being compacted)
+ *   live[n]   : nullable u8 mask (the findKey filter, bitree/bithash.go:225-228)
+ *   khash[n]  : nullable -> hash.Fnv32(userKey)
+ *   init_size, out, out_cap, o : as bhg_encode_ikey_batch
+ * A handle that is not one whole record (out of range, ikeySize < 8,
+ * 12 + ikeySize + valueSize != length) gets BHG_ST_RECORD_NIL. */
+int bhg_repack_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
+                     const uint8_t *live, const uint32_t *khash, uint32_t init_size, uint8_t *out,
+                     uint64_t out_cap, const bhg_encode_out *o, void *stream);
+
 /* ---- table tail (device): Writer.writeTable for many tables at once ----
  * Replaces writeData's empty record header, writeConflict, writeIndexHash,
  * writeMeta and writeFooter (bithash/writer.go:312-338, 393-533), with

@@ -1,0 +1,133 @@
+"""GPU compaction and iteration against the restated reference:
+
+* K4 (bithash_test.go:247-291): 102,400 records of 2 KiB in one 512 MiB
+  table written on the GPU (encode + tail), iterated back in write order by
+  the GPU scan + decode -- (userKey, seqNum, value, fileNum) per record.
+* compactBithashFiles' bithash side (bitree/bithash.go:158-270, the
+  TestBithashCompact shape bithash_test.go:150-245): source tables scanned,
+  liveness-filtered and re-packed with AddIkey semantics into one table whose
+  whole file equals the restated Writer.add_ikey + write_table output, and
+  every live key reads back through the restated Reader.Get."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle import table as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from bitalosdb_amd.codec import BithashCodec
+    c = BithashCodec(0)
+    yield c
+    c.close()
+
+
+def test_k4_compact_iter_order(codec):
+    from bitalosdb_amd.codec import as_device_bytes, _u64_tensor
+    n = 102_400
+    rng = np.random.default_rng(4)
+    blob = rng.integers(0, 256, n * 2048, dtype=np.uint8).tobytes()
+    vals = [blob[i * 2048:(i + 1) * 2048] for i in range(n)]
+    keys = [b"bithash_testkey_%d" % i for i in range(n)]
+    trs = [((i + 1) << 8) | 1 for i in range(n)]
+    files, res, stats = codec.encode_tables(keys, trs, vals, file_nums=[1], table_max=512 << 20)
+    assert list(files) == [1] and res["ntables"] == 1 and int(stats[0, 0]) == n
+    f = files[1]
+    # restated writer: the same file
+    w = T.Writer(1, 512 << 20)
+    for k, tr, v in zip(keys, trs, vals):
+        w.add(k, tr, v)
+    w.write_table(True)
+    assert f == bytes(w.file)
+    # TableIterator on the GPU: scan + decode, in write order
+    moff, _ = T.read_footer(f)
+    data_len = T.open_table(f)["data_bh"][1]
+    with torch.cuda.stream(codec.stream):
+        src_t = as_device_bytes(f, codec.device)
+        h_t, first, end = codec.scan_tables(src_t, _u64_tensor([0, data_len], codec.device), mode=0)
+        codec.sync()
+    h = h_t.cpu().numpy().view(O.HANDLE_DT).reshape(-1)
+    assert len(h) == n
+    desc, _, _ = codec.decode(f, h)
+    assert (desc["status"] == 0).all()
+    assert (desc["trailer"] >> 8 == np.arange(1, n + 1)).all() and (desc["file_num"] == 1).all()
+    fb = np.frombuffer(f, np.uint8)
+    for i in list(range(0, n, 4099)) + [n - 1]:
+        o = int(h["offset"][i])
+        assert fb[o + 12:o + 12 + int(desc["key_len"][i])].tobytes() == keys[i]
+        vo = o + int(desc["val_off"][i])
+        assert fb[vo:vo + int(desc["val_len"][i])].tobytes() == vals[i]
+    assert np.array_equal(desc["fnv1"], np.array([O.fnv32(k) for k in keys], np.uint32))
+
+
+@pytest.mark.parametrize("compressor,init", [(0, 0), (1, 0), (0, 777)])
+def test_compaction_repack_pipeline(codec, compressor, init):
+    from bitalosdb_amd.codec import as_device_bytes
+    rng = random.Random(40 + compressor + init)
+    st = T.Store(1 << 20, compressor=compressor)
+    s = st.flush_start()
+    live_keys = {}
+    for i in range(2500):
+        k = b"ck_%05d" % rng.randrange(1800)
+        s.add(k, i + 1, bytes(rng.randrange(65, 91) for _ in range(rng.choice([10, 300, 1500]))))
+    s.compact = True
+    s.finish()
+    fns = sorted(st.files)
+    blobs = [bytes(st.files[fn]) for fn in fns]
+    # data regions only (as TableIterator reads them); records in scan order
+    recs = []
+    for fn, b in zip(fns, blobs):
+        for uk, tr, v, hfn in T.table_iter(b):
+            recs.append((uk, tr, v, hfn))
+            live_keys[uk] = tr >> 8                              # the latest seqNum wins (findKey)
+    live = np.array([live_keys[uk] == tr >> 8 for uk, tr, _, _ in recs], np.uint8)
+    assert 0 < live.sum() < len(recs)
+    w = T.Writer(99, 1 << 40, compressor=compressor)
+    if init:
+        w.file += bytes(init)
+        w.current_offset = w.size = init
+    for (uk, tr, v, hfn), lv in zip(recs, live):
+        if lv:
+            w.add_ikey(uk, tr, v, O.fnv32(uk), hfn)
+    w.write_table(True)
+    want = bytes(w.file[init:])
+    src = b"".join(blobs)
+    toff = np.cumsum([0] + [len(b) for b in blobs]).tolist()
+    # the scan must stop at each table's data end, as TableIterator does
+    with torch.cuda.stream(codec.stream):
+        src_t = as_device_bytes(src, codec.device)
+    got, status, h = codec.compact(src_t, toff, live=live, init_size=init)
+    assert len(h) == len(recs)
+    assert (status[live == 1] == 0).all() and (status[live == 0] == O.SKIPPED).all()
+    assert got == want
+    if init == 0:
+        for uk, tr, v, _ in recs[::37]:
+            if live_keys[uk] == tr >> 8:
+                assert T.table_get(got, uk, compressor) == (O.snappy_decode(v) if compressor else v)
+
+
+def test_repack_bad_handles(codec):
+    """Handles that are not whole records -> RECORD_NIL, nothing written for them."""
+    from bitalosdb_amd.codec import as_device_bytes, handles_tensor
+    recs = [O.record_set(b"key%d" % i, (i + 1) << 8 | 1, b"v" * (10 + i), 7) for i in range(6)]
+    src = b"".join(recs)
+    offs = np.cumsum([0] + [len(r) for r in recs])
+    hs = [(int(offs[i]), len(recs[i]), 0) for i in range(6)]
+    hs[1] = (hs[1][0], hs[1][1] - 1, 0)              # length mismatch
+    hs[3] = (len(src) - 5, 30, 0)                    # past the end
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    with torch.cuda.stream(codec.stream):
+        src_t = as_device_bytes(src, codec.device)
+        ht = handles_tensor(h, codec.device)
+        out_t, bufs = codec.repack_batch(src_t, ht, 6)
+        codec.sync()
+    st = bufs.status.cpu().numpy().view(np.uint32)
+    assert list(st) == [0, O.RECORD_NIL, 0, O.RECORD_NIL, 0, 0]
+    size = int(bufs.table_size[0].item())
+    assert out_t[:size].cpu().numpy().tobytes() == recs[0] + recs[2] + recs[4] + recs[5]
