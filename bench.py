@@ -1,14 +1,18 @@
 #!/usr/bin/env python
 """Benchmark: GiB/s of bithash blocks decoded (device-resident), 32 B key / 1 KiB value.
 
-One "step" = one pass of the hot path (bhg_decode_batch: CRC-32C + readRecord
-validation + KV-record decode + FNV-1) over one batch of 1M synthetic blocks
-already resident in HBM (BASELINE.json configs[1]).  N GPUs (torch.distributed
-run, one rank per GPU) each decode their own tables: weak scaling, no
-data-path collective.  Rank 0 prints one JSON line.
+One "step" = one pass of the hot path (bhg_decode_batch: CRC-32C verify
+against the writer's CRCs + readRecord validation + KV-record decode + FNV-1)
+over one batch of 1M synthetic blocks already resident in HBM
+(BASELINE.json configs[1]).  N GPUs (torch.distributed run, one rank per GPU)
+each decode their own tables: weak scaling, no data-path collective.  Rank 0
+prints one JSON line.  --config c5 is the fixed 25 GB corpus (184 tables x
+124,738 blocks) split round-robin by table over the N GPUs: strong scaling.
 
 Extra legs (N=1, rank 0, outside the timed region):
-  * cpu_baseline -- the C restatement (oracle/) on the host cores, bounded sample
+  * cpu_baseline -- the C restatement (oracle/) on the host cores, bounded sample:
+                    in-memory on every usable core, 1 thread, and pread-per-block
+  * copy ceiling -- a measured device-to-device copy of the same bytes
   * e2e          -- the host-buffer path (H2D + kernel + D2H), recorded in DESIGN.md
 """
 import argparse
@@ -42,8 +46,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "scan", "scanmix", "get", "indexcrc"],
+    ap.add_argument("--codec", default="none", choices=["none", "snappy"], help="c5 only")
+    ap.add_argument("--c5-tables", type=int, default=184, help="c5 corpus size in 128 MiB tables")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "scan", "scanmix", "get", "indexcrc"],
                     help="c2: uncompressed decode (BASELINE metric); c3: snappy decode; c4: encode; "
+                         "c5: 25 GB corpus sharded round-robin by table over the GPUs (strong scaling); "
                          "scan/scanmix: table data-region scan over uniform / mixed-length tables; "
                          "get: batched Bithash.Get (HashIndex + conflict SeekGE + readData) over full tables; "
                          "indexcrc: per-table indexhash_checksum verify (masked CRC-32C of 1.51 MB per table)")
@@ -60,6 +67,29 @@ def cpu_info():
     except OSError:
         pass
     return model
+
+
+def usable_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def copy_ceiling(src_t, dev, reps=5):
+    """Measured device-to-device copy of the same bytes (read + write), GB/s."""
+    dst = torch.empty_like(src_t)
+    dst.copy_(src_t)
+    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    for i in range(reps):
+        e0[i].record()
+        dst.copy_(src_t)
+        e1[i].record()
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([x.elapsed_time(y) for x, y in zip(e0, e1)]))
+    del dst
+    return 2.0 * src_t.numel() / (ms * 1e-3) / 1e9, ms
 
 
 def pmc_traffic():
@@ -108,6 +138,8 @@ def run(a, world, rank, local, dev, codec):
         return run_get(a, world, rank, local, dev, codec)
     if a.config == "indexcrc":
         return run_indexcrc(a, world, rank, local, dev, codec)
+    if a.config == "c5":
+        return run_c5(a, world, rank, local, dev, codec)
     import torch.distributed as dist
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import handles_tensor
@@ -118,9 +150,12 @@ def run(a, world, rank, local, dev, codec):
     h_t = handles_tensor(h, dev)
     desc_t = torch.empty(n * 40, dtype=torch.uint8, device=dev)
     L = meta["rec_len"]
+    # the CRCs the writer recorded (crc.New(record).Value()), from the lane-per-range GPU primitive:
+    # the timed step is the CRC-verify path (a mismatch would flip the block to BHG_ST_CRC_MISMATCH)
+    exp_crc = codec.crc_batch(src_t, h_t, n)
 
     def step():
-        codec.decode_batch(src_t, src_t.numel(), h_t, n, out_desc=desc_t)
+        codec.decode_batch(src_t, src_t.numel(), h_t, n, expected_crc=exp_crc, out_desc=desc_t)
 
     for _ in range(a.warmup):
         step()
@@ -158,13 +193,14 @@ def run(a, world, rank, local, dev, codec):
                   ("trailer", "<u8"), ("file_num", "<u4"), ("fnv1", "<u4"), ("crc", "<u4"),
                   ("status", "<u4")]))
     ok_blocks = int((d["status"] == 0).sum())
-    digest = int(np.bitwise_xor.reduce(d["crc"].astype(np.uint64) * np.uint64(0x9E3779B1) ^ d["fnv1"]))
     from bitalosdb_amd import shard
-    elapsed, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok_blocks, n, digest & (2 ** 64 - 1), dev)
+    digest = shard.block_digest(d["crc"], d["fnv1"], d["trailer"], d["status"])
+    elapsed, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok_blocks, n, digest, dev)
+    copy_gbps, copy_ms = copy_ceiling(src_t, dev)
 
     total_blocks = n_total * a.steps
     value = total_blocks * L / elapsed / 2 ** 30
-    achieved = n * ALGO_BYTES_PER_BLOCK / (avg_kern_ms * 1e-3) / 1e9
+    achieved = n * (ALGO_BYTES_PER_BLOCK + 4) / (avg_kern_ms * 1e-3) / 1e9   # + the expected CRC read
     traffic = pmc_traffic()
     out = {
         "metric": METRIC,
@@ -179,15 +215,22 @@ def run(a, world, rank, local, dev, codec):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded torch generator; FuncRandBytes alphabet keys/values; 128 MiB tables)",
-        "config": {"workload": "BASELINE configs[1]: 1M uncompressed bithash blocks per GPU, CRC-verify + "
-                               "KV-record decode, 32B key / 1KB value",
+        "config": {"workload": "BASELINE configs[1]: 1M uncompressed bithash blocks per GPU, CRC-verify "
+                               "(expected_crc) + KV-record decode, 32B key / 1KB value",
                    "blocks_per_gpu": n, "record_bytes": L, "tables_per_gpu": meta["tables"],
                    "codec": "none", "parallelism": "table-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "traffic_source": "not measured in this run: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of "
+                                       "the same command, committed in profiles/pmc_decode_c2.json",
                      "kernel": "k_decode_tile<8>", "kernel_avg_ms": round(avg_kern_ms, 4),
-                     "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK},
+                     "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK + 4,
+                     "measured_copy_ceiling": {"GBps": round(copy_gbps, 1), "ms": round(copy_ms, 4),
+                                               "what": "torch D2D copy of the same %d B (read + write)"
+                                                       % src_t.numel(),
+                                               "frac_of_copy": round(achieved / copy_gbps, 4)}},
         "status_ok_blocks": int(ok_total),
+        "valid": bool(ok_total == n_total),
         "digest_all_ranks": "%016x" % digest_all,
     }
 
@@ -221,27 +264,52 @@ def run(a, world, rank, local, dev, codec):
         from oracle import oracle as O
         if host_src is None:
             host_src = src_t.cpu().numpy()
-        threads = min(16, os.cpu_count() or 1)
-        # parity on the measured batch (restatement vs device descriptors)
-        exp, _, _ = O.decode_batch(host_src, h, nthreads=threads)
+        threads = usable_cores()
+        exp_host = exp_crc.cpu().numpy().view(np.uint32)
+        # parity on the measured batch (restatement vs device descriptors, same expected CRCs)
+        exp, _, _ = O.decode_batch(host_src, h, expected_crc=exp_host, nthreads=threads)
         parity = all(np.array_equal(exp[f], d[f]) for f in d.dtype.names)
+        budget = a.cpu_seconds / 3
         reps, t = 0, time.perf_counter()
         while True:
-            O.decode_batch(host_src, h, nthreads=threads)
+            O.decode_batch(host_src, h, expected_crc=exp_host, nthreads=threads)
             reps += 1
-            if time.perf_counter() - t >= a.cpu_seconds:
+            if time.perf_counter() - t >= budget:
                 break
         cpu_s = time.perf_counter() - t
         m1 = min(n, 200_000)
         t = time.perf_counter()
-        O.decode_batch(host_src, h[:m1], nthreads=1)
+        O.decode_batch(host_src, h[:m1], expected_crc=exp_host[:m1], nthreads=1)
         st_s = time.perf_counter() - t
+        # Reader.readData's shape: one pread per block from the table file (page cache)
+        import tempfile
+        fd, path = tempfile.mkstemp(prefix="bhg_c2_", dir="/tmp")
+        try:
+            with os.fdopen(os.dup(fd), "wb") as f:
+                host_src.tofile(f)
+            preps, t = 0, time.perf_counter()
+            while True:
+                pd = O.decode_batch_pread(fd, h, expected_crc=exp_host, nthreads=threads)
+                preps += 1
+                if time.perf_counter() - t >= budget:
+                    break
+            pr_s = time.perf_counter() - t
+            pread_ok = bool(np.array_equal(pd["crc"], d["crc"]) and np.array_equal(pd["status"], d["status"]))
+        finally:
+            os.close(fd)
+            os.unlink(path)
         out["cpu_baseline"] = {
             "value": round(reps * n * L / cpu_s / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": "C restatement of readData/readRecord + masked CRC-32C (SSE4.2) + FNV-1 over the same %d "
-                      "blocks, %d passes in %.1f s on %d threads (%s); 1 thread: %.3f GiB/s"
-                      % (n, reps, cpu_s, threads, cpu_info(), m1 * L / st_s / 2 ** 30)}
+            "sample": "C restatement of readData/readRecord + masked CRC-32C verify (SSE4.2) + FNV-1 over the same "
+                      "%d blocks in memory, %d passes in %.1f s on %d threads = every core this process may use "
+                      "(os.cpu_count() %d; %s)" % (n, reps, cpu_s, threads, os.cpu_count() or 0, cpu_info()),
+            "one_thread": round(m1 * L / st_s / 2 ** 30, 3),
+            "pread_per_block": {"value": round(preps * n * L / pr_s / 2 ** 30, 3), "threads": threads,
+                                "matches_device_path": pread_ok,
+                                "note": "one pread() of bh.Length bytes per block from the table file in the page "
+                                        "cache, as Reader.readData's ReadAt (reader.go:251)"}}
         out["parity_vs_restatement"] = "bit-exact" if parity else "MISMATCH"
+        out["valid"] = bool(out["valid"] and parity)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -400,6 +468,169 @@ def run_c4(a, world, rank, local, dev, codec):
         res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+C5_RECORDS_PER_TABLE = 124_738      # 128 MiB / 1076 B, the add that crosses the limit included
+
+
+def _c5_snappy_tables(codec, owned, R, dev, seed):
+    """The owned tables of the C5 corpus in the snappy variant: table t's
+    R values (SURVEY §8d C3 generator, seeded per table) encoded on the GPU
+    into one table file data region (fileNum 1 + t, seqNums t*R+1..).
+    Returns (src, handles HANDLE_DT, expected CRCs int32 tensor, raw value bytes)."""
+    from bitalosdb_amd import synth
+    from bitalosdb_amd.codec import EncodeBuffers, HANDLE_DT
+    parts, hs, crcs = [], [], []
+    base, raw = 0, 0
+    for t in owned:
+        ts = synth.table_seed(seed, t)
+        keys = synth.keys_gpu(R, device=dev, seed=ts).reshape(-1).contiguous()
+        key_off = torch.arange(0, (R + 1) * 32, 32, dtype=torch.int64, device=dev)
+        tr = ((torch.arange(t * R + 1, (t + 1) * R + 1, dtype=torch.int64, device=dev)) << 8) | 1
+        vals = synth.compressible_values_gpu(R, 1024, device=dev, seed=ts + 1).reshape(-1).contiguous()
+        val_off = torch.arange(0, (R + 1) * 1024, 1024, dtype=torch.int64, device=dev)
+        out = torch.empty(R * 64 + vals.numel() * 7 // 6 + 64, dtype=torch.uint8, device=dev)
+        bufs = EncodeBuffers(R, 1, dev)
+        fns = torch.tensor([1 + t], dtype=torch.int32, device=dev)
+        codec.encode_batch(keys, key_off, tr, vals, val_off, R, 1, fns, 1, 0, 1 << 30, out, bufs,
+                           vals_len=vals.numel())
+        codec.sync()
+        size = int(bufs.table_size[0].item())
+        parts.append(out[:size + 12].clone())
+        parts[-1][size:] = 0                               # writeData's empty record header
+        h = np.zeros(R, dtype=HANDLE_DT)
+        h["offset"] = bufs.pos.cpu().numpy().view(np.uint64) + np.uint64(base)
+        h["length"] = bufs.bh_len.cpu().numpy().view(np.uint32)
+        hs.append(h)
+        crcs.append(bufs.crc.clone())
+        base += size + 12
+        raw += vals.numel()
+        del keys, vals, out, bufs
+    return torch.cat(parts), np.concatenate(hs), torch.cat(crcs), raw
+
+
+def run_c5(a, world, rank, local, dev, codec):
+    """BASELINE configs[4]: a fixed 25 GB corpus of bithash table files (184
+    tables x 124,738 blocks of 32 B key / 1 KiB value), table t decoded by
+    rank t mod N (round-robin by table file).  Each rank decodes
+    all of its tables in one bhg_decode_batch per step (CRC verify against
+    the writer's CRCs + record decode, snappy decompress for --codec snappy);
+    no data-path collective.  value = corpus bytes / max-over-ranks time:
+    strong scaling, every N decodes the same 25 GB."""
+    import torch.distributed as dist
+    from bitalosdb_amd import shard, synth
+    from bitalosdb_amd.codec import handles_tensor
+    T, R = a.c5_tables, C5_RECORDS_PER_TABLE
+    owned = shard.owned_tables(T, world, rank)
+    snappy = a.codec == "snappy"
+    t_build = time.perf_counter()
+    if snappy:
+        src_t, h, exp_crc, raw = _c5_snappy_tables(codec, owned, R, dev, synth.SEED)
+    else:
+        src_t, h, meta = synth.table_set(owned, R, device=dev, seed=synth.SEED, first_file_num=1)
+        raw = len(h) * 1024
+    n = len(h)
+    h_t = handles_tensor(h, dev)
+    if not snappy:
+        exp_crc = codec.crc_batch(src_t, h_t, n)
+    desc_t = torch.empty(max(n, 1) * 40, dtype=torch.uint8, device=dev)
+    vals_t = torch.empty(max(n, 1) * 1024 + 64, dtype=torch.uint8, device=dev) if snappy else None
+    voff_t = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev) if snappy else None
+    torch.cuda.synchronize(dev)
+    build_s = time.perf_counter() - t_build
+    disk = float(h["length"].astype(np.float64).sum())
+
+    def step():
+        if n:
+            codec.decode_batch(src_t, src_t.numel(), h_t, n, 1 if snappy else 0, expected_crc=exp_crc,
+                               out_desc=desc_t, out_vals=vals_t, out_val_off=voff_t)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    for i in range(a.steps):
+        e0[i].record()
+        step()
+        e1[i].record()
+    torch.cuda.synchronize(dev)
+    step_ms = float(np.mean([x.elapsed_time(y) for x, y in zip(e0, e1)])) if n else 0.0
+    d = desc_t[:n * 40].cpu().numpy().view(DESC_DT)
+    ok = int((d["status"] == 0).sum())
+    digest = shard.block_digest(d["crc"], d["fnv1"], d["trailer"], d["status"])
+    el_max, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok, n, digest, dev)
+    dt = torch.tensor([disk, raw], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt)
+    disk_total, raw_total = float(dt[0].item()), float(dt[1].item())
+    value = disk_total * a.steps / el_max / 2 ** 30
+    # per-GPU roofline of this rank's step: algorithmic bytes (handle + record + descriptor + expected CRC,
+    # + decoded value bytes written for snappy) over the event-timed step
+    algo = n * (16 + 40 + 4) + disk + (raw if snappy else 0)
+    achieved = algo / (step_ms * 1e-3) / 1e9 if step_ms else 0.0
+    out = {
+        "metric": "GiB/s bithash table files decoded (device-resident), 25 GB corpus sharded by table, "
+                  "32B key / 1KB value",
+        "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(el_max / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (per-table seeded generator: a table's bytes do not depend on N)",
+        "config": {"workload": "BASELINE configs[4]: %d tables x %d blocks (%.2f GB on disk), table t -> rank t "
+                               "mod %d, CRC-verify + record decode%s" % (T, R, disk_total / 1e9, world,
+                                                                        " + snappy decompress" if snappy else ""),
+                   "codec": a.codec, "tables": T, "tables_this_rank": len(owned), "blocks_total": int(n_total),
+                   "parallelism": "table-sharded x%d" % world, "corpus_build_s": round(build_s, 2)},
+        "per_gpu_GiBps": round(value / world, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "scope": "rank 0, per GPU",
+                     "step_avg_ms": round(step_ms, 4)},
+        "status_ok_blocks": int(ok_total), "valid": bool(ok_total == n_total == T * R),
+        "digest_all_ranks": "%016x" % digest_all,
+    }
+    if snappy:
+        out["decoded_GiBps"] = round(raw_total * a.steps / el_max / 2 ** 30, 3)
+    if rank == 0 and world == 1 and not a.no_cpu and n:
+        from oracle import oracle as O
+        # parity + baseline on a bounded sample: the first table (the restatement decodes it bit for bit)
+        first = np.nonzero(h["offset"] >= 0)[0][:R]
+        hs = h[first]
+        lo = int(hs["offset"].min())
+        hi = int((hs["offset"] + hs["length"]).max())
+        host = src_t[lo:hi].cpu().numpy()
+        hr = hs.copy()
+        hr["offset"] -= np.uint64(lo)
+        ecrc = exp_crc[:R].cpu().numpy().view(np.uint32)
+        threads = usable_cores()
+        e, _, _ = O.decode_batch(host, hr, codec=1 if snappy else 0, expected_crc=ecrc, nthreads=threads)
+        dd = d[:R]
+        fields = [f for f in DESC_DT.names if not (snappy and f == "val_off")]
+        par = all(np.array_equal(e[f], dd[f]) for f in fields)
+        reps, t = 0, time.perf_counter()
+        while time.perf_counter() - t < a.cpu_seconds:
+            O.decode_batch(host, hr, codec=1 if snappy else 0, expected_crc=ecrc, nthreads=threads)
+            reps += 1
+        cs = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": round(reps * (hi - lo) / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": threads,
+                               "kind": "port", "sample": "C restatement over table 0 (%d blocks, %d B), %d passes on "
+                                                         "%d threads (%s)" % (R, hi - lo, reps, threads, cpu_info())}
+        out["parity_table0_vs_restatement"] = "bit-exact" if par else "MISMATCH"
+        out["valid"] = bool(out["valid"] and par)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def run_scan(a, world, rank, local, dev, codec):

@@ -24,9 +24,24 @@ def shard_handles(handles, table_of_handle, world, rank):
     return handles[mask]
 
 
+def block_digest(crc, fnv1, trailer, status):
+    """Order- and partition-independent digest of decoded blocks: the 64-bit mix
+    of each block's (crc, fnv1, trailer, status), summed as two independent
+    32-bit lanes mod 2^32 -- per-rank digests add up (reduce_stats) to the
+    single-process digest of the same blocks."""
+    m = (np.asarray(crc, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ \
+        (np.asarray(fnv1, np.uint64) << np.uint64(17)) ^ np.asarray(trailer, np.uint64) ^ \
+        (np.asarray(status, np.uint64) << np.uint64(40))
+    m = m * np.uint64(0xBF58476D1CE4E5B9)
+    m ^= m >> np.uint64(31)
+    lo = int((m & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)) & 0xFFFFFFFF
+    hi = int((m >> np.uint64(32)).sum(dtype=np.uint64)) & 0xFFFFFFFF
+    return lo | (hi << 32)
+
+
 def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
-    """MAX of elapsed, SUM of block counts, XOR-fold of per-rank digests (as sum of
-    64-bit halves mod 2^32 pairs); returns python values.  Runs outside the timed region."""
+    """MAX of elapsed, SUM of block counts, per-rank digests added as two 32-bit
+    lanes mod 2^32 (block_digest); returns python values.  Runs outside the timed region."""
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
     c = torch.tensor([ok_blocks, n_blocks, digest & 0xFFFFFFFF, digest >> 32], dtype=torch.int64, device=device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:

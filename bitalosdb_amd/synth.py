@@ -70,6 +70,50 @@ def uniform_tables(n, key_len=32, val_len=1024, device="cuda", seed=SEED, table_
     return src, h, meta
 
 
+def table_seed(seed, t):
+    """Generator seed of table t: a table's bytes depend only on (seed, t), so a
+    table decodes to the same descriptors whichever rank materialises it."""
+    return (int(seed) * 1_000_003 + 7919 * int(t)) & ((1 << 63) - 1)
+
+
+def table_set(table_ids, records_per_table, key_len=32, val_len=1024, device="cuda", seed=SEED, first_file_num=1,
+              chunk=1 << 16):
+    """The tables `table_ids` of a fixed corpus (table t holds
+    records t*R+1 .. (t+1)*R as seqNums, file number first_file_num + t),
+    concatenated in the order given.  Returns (src uint8 tensor, handles HANDLE_DT,
+    meta); table j of the list starts at j * table_bytes."""
+    from ._lib import HANDLE_DT
+    device = torch.device(device)
+    klen = key_len + 8
+    L = 12 + klen + val_len
+    R = int(records_per_table)
+    tbytes = R * L + 12
+    src = torch.zeros(len(table_ids) * tbytes, dtype=torch.uint8, device=device)
+    alpha = _alpha(device)
+    hdr = np.zeros(12, dtype=np.uint8)
+    for j, t in enumerate(table_ids):
+        g = torch.Generator(device=device)
+        g.manual_seed(table_seed(seed, t))
+        view = src[j * tbytes:j * tbytes + R * L].view(R, L)
+        hdr[:] = np.frombuffer(np.array([klen, val_len, first_file_num + t], dtype="<u4").tobytes(), dtype=np.uint8)
+        view[:, :12] = torch.from_numpy(hdr.copy()).to(device)
+        for c0 in range(0, R, chunk):
+            c1 = min(R, c0 + chunk)
+            m = c1 - c0
+            view[c0:c1, 12:12 + key_len] = _rand_alpha(g, (m, key_len), device, alpha)
+            seq = torch.arange(t * R + c0 + 1, t * R + c1 + 1, device=device, dtype=torch.int64)
+            view[c0:c1, 12 + key_len:12 + klen] = ((seq << 8) | 1).view(torch.uint8).view(m, 8)
+            view[c0:c1, 12 + klen:] = _rand_alpha(g, (m, val_len), device, alpha)
+    n = len(table_ids) * R
+    h = np.zeros(n, dtype=HANDLE_DT)
+    i = np.arange(n, dtype=np.uint64)
+    h["offset"] = (i // R) * np.uint64(tbytes) + (i % R) * np.uint64(L)
+    h["length"] = L
+    meta = dict(n=n, rec_len=L, records_per_table=R, tables=len(table_ids), table_bytes=tbytes,
+                src_bytes=int(src.numel()), block_bytes=n * L, table_ids=list(table_ids))
+    return src, h, meta
+
+
 def compressible_values(rng, n_vals, val_len, dict_size=4096, fresh=0.2):
     """Values of tokens (4-64 B) drawn from a seeded dictionary, ~20 % fresh
     random bytes -- the SURVEY §8d C3 generator (numpy, host)."""

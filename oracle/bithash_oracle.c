@@ -9,6 +9,7 @@
 #include "bithash_oracle.h"
 
 #include <pthread.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 #if defined(__x86_64__)
@@ -364,6 +365,49 @@ void bho_decode_batch(const uint8_t *src, uint64_t src_len, const bho_handle *h,
     }
     if (nt == 1) { dec_worker(&jobs[0]); return; }
     for (int t = 0; t < nt; t++) pthread_create(&tid[t], NULL, dec_worker, &jobs[t]);
+    for (int t = 0; t < nt; t++) pthread_join(tid[t], NULL);
+}
+
+/* Reader.readData as the reference runs it (reader.go:251): one ReadAt
+ * (pread) of bh.Length bytes per block into a buffer, then readRecord /
+ * Decode on that buffer.  A short read -> ErrBhReadAtIncomplete
+ * (BHO_INCOMPLETE).  Baseline mode only (SSE4.2 CRC), codec NONE. */
+typedef struct {
+    int fd; const bho_handle *h; uint32_t lo, hi; const uint32_t *expected_crc; bho_desc *out;
+} pread_job;
+
+static void *pread_worker(void *arg) {
+    pread_job *j = (pread_job *)arg;
+    size_t cap = 1 << 16;
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    for (uint32_t i = j->lo; i < j->hi && buf; i++) {
+        const bho_handle *h = j->h + i;
+        if (h->length > cap) {
+            free(buf);
+            cap = h->length;
+            buf = (uint8_t *)malloc(cap);
+            if (!buf) break;
+        }
+        ssize_t got = h->length ? pread(j->fd, buf, h->length, (off_t)h->offset) : 0;
+        if (got < 0) got = 0;
+        bho_handle local = {0, h->length, 0};
+        decode_one(buf, (uint64_t)got, &local, 0, j->expected_crc, i, j->out + i, NULL, NULL, 1);
+    }
+    free(buf);
+    return NULL;
+}
+
+void bho_decode_batch_pread(int fd, const bho_handle *h, uint32_t n, const uint32_t *expected_crc, bho_desc *out,
+                            int nthreads) {
+    int nt = nthreads < 1 ? 1 : nthreads;
+    if (nt > 256) nt = 256;
+    pthread_t tid[256];
+    pread_job jobs[256];
+    for (int t = 0; t < nt; t++)
+        jobs[t] = (pread_job){fd, h, (uint32_t)((uint64_t)n * t / nt), (uint32_t)((uint64_t)n * (t + 1) / nt),
+                              expected_crc, out};
+    if (nt == 1) { pread_worker(&jobs[0]); return; }
+    for (int t = 0; t < nt; t++) pthread_create(&tid[t], NULL, pread_worker, &jobs[t]);
     for (int t = 0; t < nt; t++) pthread_join(tid[t], NULL);
 }
 

@@ -80,6 +80,11 @@ size_t bho_record_set(uint8_t *dst, const uint8_t *ukey, size_t uklen, uint64_t 
 void bho_decode_batch(const uint8_t *src, uint64_t src_len, const bho_handle *h, uint32_t n,
                       int codec, const uint32_t *expected_crc, bho_desc *out,
                       uint8_t *out_vals, const uint64_t *out_val_off, int nthreads);
+/* Reader.readData with one pread() per block into a buffer (reader.go:251),
+ * codec 0, SSE4.2 CRC: the CPU baseline that pays the reference's per-block
+ * ReadAt.  fd is an open descriptor of the table bytes. */
+void bho_decode_batch_pread(int fd, const bho_handle *h, uint32_t n, const uint32_t *expected_crc, bho_desc *out,
+                            int nthreads);
 /* snappy decoded sizes (0 for blocks whose header / varint is invalid) */
 void bho_decode_sizes(const uint8_t *src, uint64_t src_len, const bho_handle *h, uint32_t n,
                       uint64_t *out_sizes);

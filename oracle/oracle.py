@@ -58,6 +58,8 @@ def lib():
         L.bho_record_set.argtypes = [P, P, SZ, U64, P, SZ, U32]
         L.bho_decode_batch.restype = None
         L.bho_decode_batch.argtypes = [P, U64, P, U32, I, P, P, P, P, I]
+        L.bho_decode_batch_pread.restype = None
+        L.bho_decode_batch_pread.argtypes = [I, P, U32, P, P, I]
         L.bho_decode_sizes.restype = None
         L.bho_decode_sizes.argtypes = [P, U64, P, U32, P]
         L.bho_encode_batch.restype = I
@@ -175,6 +177,16 @@ def decode_batch(src, handles, codec=0, expected_crc=None, nthreads=0, out_val_o
     lib().bho_decode_batch(_ptr(src), src.size, _ptr(handles), n, codec, _ptr(exp), _ptr(desc),
                            _ptr(vals), _ptr(out_val_off), nthreads)
     return desc, vals, out_val_off
+
+
+def decode_batch_pread(fd, handles, expected_crc=None, nthreads=1):
+    """Reader.readData with one pread per block (reader.go:251), codec NONE,
+    baseline mode.  fd: an open file descriptor of the table bytes."""
+    handles = np.ascontiguousarray(handles, dtype=HANDLE_DT)
+    desc = np.zeros(len(handles), dtype=DESC_DT)
+    exp = None if expected_crc is None else np.ascontiguousarray(expected_crc, dtype=np.uint32)
+    lib().bho_decode_batch_pread(fd, _ptr(handles), len(handles), _ptr(exp), _ptr(desc), nthreads)
+    return desc
 
 
 def encode_batch(keys, trailers, values, codec=0, file_nums=(1,), init_size=0, table_max=128 << 20):

@@ -1,5 +1,8 @@
-"""N>1 path on CPU: world_size-2 gloo run of the table sharding + stats
-reduction that bench.py uses over RCCL on the GPU node."""
+"""N>1 path on CPU: world_size-2 gloo runs of the C5 sharding bench.py uses
+over RCCL on the GPU node -- round-robin table ownership, each rank decoding
+its own tables (the C restatement stands in for the GPU here), and the
+MAX-time / SUM-count / digest reduction, which must equal one process
+decoding every table."""
 import os
 import socket
 
@@ -32,6 +35,53 @@ def _worker(rank, world, port, q):
     el, ok, n, dg = shard.reduce_stats(0.5 + rank, len(sub), len(sub), 1000 + rank, torch.device("cpu"))
     q.put((rank, mine, len(sub), el, ok, n, dg))
     dist.destroy_process_group()
+
+
+N_TABLES, R = 9, 300
+
+
+def _decode_digest(table_ids):
+    """Materialise tables `table_ids` of the fixed corpus on the CPU and decode
+    them with the restatement: (ok blocks, n blocks, digest)."""
+    import torch
+    from bitalosdb_amd import synth
+    from oracle import oracle as O
+    src, h, meta = synth.table_set(table_ids, R, key_len=32, val_len=200, device="cpu")
+    d, _, _ = O.decode_batch(src.numpy(), h)
+    return int((d["status"] == 0).sum()), len(h), shard.block_digest(d["crc"], d["fnv1"], d["trailer"], d["status"])
+
+
+def _c5_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = shard.owned_tables(N_TABLES, world, rank)
+    ok, n, dg = _decode_digest(mine)
+    el, ok_all, n_all, dg_all = shard.reduce_stats(0.25 * (rank + 1), ok, n, dg, torch.device("cpu"))
+    q.put((rank, mine, n, el, ok_all, n_all, dg_all))
+    dist.destroy_process_group()
+
+
+def test_world2_gloo_c5_decode_digest():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_c5_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    ok1, n1, dg1 = _decode_digest(list(range(N_TABLES)))         # one process, every table
+    (r0, m0, nr0, el0, oka, na, dga), (r1, m1, nr1, el1, okb, nb, dgb) = res
+    assert m0 == [0, 2, 4, 6, 8] and m1 == [1, 3, 5, 7]
+    assert nr0 == 5 * R and nr1 == 4 * R
+    assert el0 == el1 == 0.5
+    assert oka == okb == ok1 == n1 == na == nb == N_TABLES * R
+    assert dga == dgb == dg1
 
 
 def test_world2_gloo_sharding():
