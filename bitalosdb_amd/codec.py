@@ -28,7 +28,7 @@ SnappyCompressor = CODEC_SNAPPY
 # Go sentinel errors each per-block status maps onto (bithash/error.go, golang/snappy)
 STATUS_ERRORS = {
     B.ST_RECORD_NIL: "bithash: read record nil",                 # ErrBhReadRecordNil
-    B.ST_ILLEGAL_LENGTH: "bithash: illegal block length",        # ErrBhIllegalBlockLength
+    B.ST_ILLEGAL_LENGTH: "bithash: illegal block handle length", # ErrBhIllegalBlockLength
     B.ST_INCOMPLETE: "bithash: readAt incomplete",               # ErrBhReadAtIncomplete / io.EOF
     B.ST_SNAPPY_CORRUPT: "snappy: corrupt input",                # snappy.ErrCorrupt
     B.ST_SNAPPY_TOO_LARGE: "snappy: decoded block is too large",

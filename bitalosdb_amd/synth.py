@@ -164,23 +164,12 @@ def keys_gpu(n, key_len=32, device="cuda", seed=SEED + 1):
     return _rand_alpha(g, (n, key_len), device, _alpha(device))
 
 
-class _HostKeys:
-    """keys[i] -> user key bytes of record i, read from a host copy of src (only
-    touched for repeated hashes by table.update_hash_groups)."""
-
-    def __init__(self, host, offsets, key_len):
-        self.host, self.off, self.kl = host, offsets, key_len
-
-    def __getitem__(self, i):
-        o = int(self.off[i]) + 12
-        return self.host[o:o + self.kl].tobytes()
-
-
 def full_tables(codec, n, key_len=32, val_len=1024, seed=SEED, table_max=TABLE_MAX, first_file_num=1):
-    """uniform_tables() closed into complete .bht files (Writer.writeTable tails:
-    conflict / indexhash / meta / footer, bitalosdb_amd.table.table_tail), the
-    FNV-1 of every key taken from one GPU decode pass and the indexhash
-    checksum from the GPU CRC primitive.
+    """uniform_tables() closed into complete .bht files: every table's
+    Writer.writeTable tail (conflict / indexhash / meta / footer) built on the
+    GPU by bhg_table_tail from the records, their FNV-1 (one GPU decode pass)
+    and table-relative handles; then NewReader's footer/meta parse on the host
+    (table.open_table).
 
     Returns (src uint8 tensor of the concatenated files, TABLE_DT records,
     handles HANDLE_DT rebased to src, meta)."""
@@ -190,28 +179,31 @@ def full_tables(codec, n, key_len=32, val_len=1024, seed=SEED, table_max=TABLE_M
     device = codec.device
     src0, h0, meta = uniform_tables(n, key_len, val_len, device=device, seed=seed, table_max=table_max,
                                     first_file_num=first_file_num)
-    res = codec.decode_batch(src0, src0.numel(), handles_tensor(h0, device), n)
-    codec.sync()
-    fnv = res.desc_np()["fnv1"]
-    host = src0.cpu().numpy()
-    del src0
     R, L, tb = meta["records_per_table"], meta["rec_len"], meta["table_bytes"]
+    ntab = meta["tables"]
+    h0_t = handles_tensor(h0, device)
+    res = codec.decode_batch(src0, src0.numel(), h0_t, n)
+    i = torch.arange(n, device=device, dtype=torch.int64)
+    bh_off = ((i % R) * L).to(torch.int32)
+    table = (i // R).to(torch.int32)
+    fnv = res.desc.view(-1, 40)[:, 28:32].contiguous().view(torch.int32).reshape(-1)
+    counts = [min(n, (t + 1) * R) - t * R for t in range(ntab)]
+    data_end = torch.tensor([c * L for c in counts], dtype=torch.int64, device=device)
+    tail, toff, tlen, _ = codec.table_tail(src0, h0_t, bh_off, fnv, table, None, n, ntab, data_end)
+    codec.sync()
+    toff, tlen = toff.cpu().numpy(), tlen.cpu().numpy()
     parts, recs = [], []
     base = 0
     h = h0.copy()
-    for t in range(meta["tables"]):
-        r0, r1 = t * R, min(n, (t + 1) * R)
-        data_end = (r1 - r0) * L
-        bh_off = np.arange(r1 - r0, dtype=np.uint64) * np.uint64(L)
-        keys = _HostKeys(host, h0["offset"][r0:r1], key_len)
-        tail = BT.table_tail(data_end, bh_off, np.full(r1 - r0, L, np.uint64), fnv[r0:r1], keys,
-                             codec.crc_masked_bytes)
-        f = np.concatenate([host[t * tb:t * tb + data_end], np.frombuffer(tail, np.uint8)])
-        rec, _ = BT.open_table(f, base=base)
+    for t in range(ntab):
+        de = counts[t] * L
+        f = torch.cat([src0[t * tb:t * tb + de], tail[int(toff[t]):int(toff[t]) + int(tlen[t])]])
+        rec, _ = BT.open_table(f.cpu().numpy(), base=base)
         recs.append(rec)
-        h["offset"][r0:r1] = np.uint64(base) + bh_off
+        r0 = t * R
+        h["offset"][r0:r0 + counts[t]] = np.uint64(base) + np.arange(counts[t], dtype=np.uint64) * np.uint64(L)
         parts.append(f)
-        base += len(f)
-    src = torch.from_numpy(np.concatenate(parts)).to(device)
-    meta = dict(meta, src_bytes=base, table_files=[len(p) for p in parts])
+        base += int(f.numel())
+    src = torch.cat(parts)
+    meta = dict(meta, src_bytes=base, table_files=[int(p.numel()) for p in parts])
     return src, np.array(recs, dtype=TABLE_DT), h, meta
