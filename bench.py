@@ -325,22 +325,7 @@ def _pack_values(vals_t):
 def _encode_inputs(n, val_lens, dev, seed):
     """Keys/trailers/values for n pairs (values from the compressible generator)."""
     from bitalosdb_amd import synth
-    keys = synth.keys_gpu(n, device=dev, seed=seed)
-    key_off = torch.arange(0, (n + 1) * 32, 32, dtype=torch.int64, device=dev)
-    tr = (torch.arange(1, n + 1, dtype=torch.int64, device=dev) << 8) | 1
-    maxlen = int(val_lens.max().item())
-    # ragged values: value i is the first val_lens[i] bytes of row i (row-major masked_select = concatenation)
-    val_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    val_off[1:] = torch.cumsum(val_lens, 0)
-    parts = []
-    chunk = 1 << 16
-    cols = torch.arange(maxlen, device=dev)
-    for c0 in range(0, n, chunk):
-        m = min(chunk, n - c0)
-        raw = synth.compressible_values_gpu(m, maxlen, device=dev, seed=seed + c0)
-        parts.append(torch.masked_select(raw, cols.unsqueeze(0) < val_lens[c0:c0 + m].unsqueeze(1)))
-    vals = torch.cat(parts)
-    return keys.reshape(-1).contiguous(), key_off, tr, vals, val_off
+    return synth.kv_pairs_gpu(n, val_lens, device=dev, seed=seed)
 
 
 def _encode_tables(codec, n, val_lens, dev, seed, compressor):

@@ -157,6 +157,30 @@ def compressible_values_gpu(n, val_len, device="cuda", seed=SEED, words=8, word_
     return out[:, :val_len]
 
 
+def kv_pairs_gpu(n, val_lens, device="cuda", seed=SEED, key_len=32):
+    """n (key, trailer, value) inputs of a BithashWriter.Add batch built in HBM:
+    key_len-byte alphabet keys, seqNums 1..n, value i = the first val_lens[i]
+    bytes of a compressible row (compressible_values_gpu).  Returns device
+    tensors (keys, key_off[n+1], trailers, vals, val_off[n+1])."""
+    device = torch.device(device)
+    keys = keys_gpu(n, key_len=key_len, device=device, seed=seed)
+    key_off = torch.arange(0, (n + 1) * key_len, key_len, dtype=torch.int64, device=device)
+    tr = (torch.arange(1, n + 1, dtype=torch.int64, device=device) << 8) | 1
+    val_lens = val_lens.to(device=device, dtype=torch.int64)
+    maxlen = int(val_lens.max().item()) if n else 1
+    val_off = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    val_off[1:] = torch.cumsum(val_lens, 0)
+    parts = []
+    chunk = 1 << 16
+    cols = torch.arange(maxlen, device=device)
+    for c0 in range(0, n, chunk):          # ragged values: row-major masked_select = concatenation
+        m = min(chunk, n - c0)
+        raw = compressible_values_gpu(m, maxlen, device=device, seed=seed + c0)
+        parts.append(torch.masked_select(raw, cols.unsqueeze(0) < val_lens[c0:c0 + m].unsqueeze(1)))
+    vals = torch.cat(parts) if parts else torch.zeros(1, dtype=torch.uint8, device=device)
+    return keys.reshape(-1).contiguous(), key_off, tr, vals, val_off
+
+
 def keys_gpu(n, key_len=32, device="cuda", seed=SEED + 1):
     device = torch.device(device)
     g = torch.Generator(device=device)

@@ -1,0 +1,44 @@
+#!/usr/bin/env python
+"""Per-launch HBM traffic of one kernel from scripts/profile_bench.sh output.
+
+FETCH_SIZE x2 (gfx950 counts wide streaming reads at half their bytes,
+/opt/skills/guides/MI355X_MICROARCH.md "HBM / rocprofv3"), WRITE_SIZE x1,
+KiB -> bytes; plus the kernel's average duration from the trace pass.
+usage: scripts/pmc_summary.py <gpurun_out/tag> <kernel-name-substring> [out.json]"""
+import csv
+import glob
+import json
+import sys
+
+
+def rows(pattern):
+    for f in glob.glob(pattern, recursive=True):
+        yield from csv.DictReader(open(f))
+
+
+def main():
+    d, kname = sys.argv[1], sys.argv[2]
+    vals = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        v = [float(r["Counter_Value"]) for r in rows(d + "/pmc_%s/**/*counter_collection.csv" % c)
+             if kname in r["Kernel_Name"] and r["Counter_Name"] == c]
+        vals[c] = (sum(v) / len(v), len(v)) if v else (None, 0)
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(d + "/trace/**/*kernel_trace.csv")
+            if kname in r["Kernel_Name"]]
+    fetch, wr = vals["FETCH_SIZE"][0], vals["WRITE_SIZE"][0]
+    out = {"kernel": kname, "launches": [vals["FETCH_SIZE"][1], vals["WRITE_SIZE"][1]],
+           "fetch_size_kib": fetch, "write_size_kib": wr,
+           "read_bytes_per_launch": None if fetch is None else fetch * 1024 * 2,
+           "write_bytes_per_launch": None if wr is None else wr * 1024,
+           "hbm_bytes_per_launch": None if fetch is None or wr is None else fetch * 2048 + wr * 1024,
+           "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE x1; KiB -> bytes",
+           "trace_launches": len(durs), "trace_avg_ms": (sum(durs) / len(durs) / 1e6) if durs else None,
+           "trace_min_ms": (min(durs) / 1e6) if durs else None, "source": d}
+    s = json.dumps(out, indent=1)
+    print(s)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
