@@ -171,7 +171,6 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
         const uint32_t status = dw[9];
         if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
         const uint32_t cpos = dw[2], dlen = dw[3];  // provisional: value position in the record, decoded length
-        if (cpos == 0) continue;                    // finalized by k_snappy_lds
         const bhg_handle h = handles[i];
         const uint64_t rec = base + h.offset;
         const uint32_t clen = h.length - cpos;
@@ -196,164 +195,8 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_snappy_lds: the same decode with each block staged in LDS and its
-// elements moved by a group of G = 16 lanes.  A wave decodes 4 blocks at a
-// time; each group owns a SLOT-byte LDS slot holding the block's stream
-// (loaded with 16-B coalesced reads) and, 16-B aligned after it, the decoded
-// bytes.  Every lane of a group parses the same tag (LDS broadcast reads, no
-// divergence inside a group), then the element's bytes move one per lane per
-// step: out[d + k] = literal ? stream[s + k] : out[d - o + (k mod o)] -- the
-// LZ77 overlap of a copy with o < length reads only bytes below d, which are
-// final, so the lanes of a step are independent.  The decoded block leaves
-// LDS as 16-B stores.  Blocks that do not fit a slot are left for
-// k_snappy_rt (their provisional descriptor is untouched).
-// ---------------------------------------------------------------------------
-template <int SLOT, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
-                                                         const bhg_handle *__restrict__ handles, uint32_t n,
-                                                         bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
-                                                         uint64_t out_cap, const uint64_t *__restrict__ val_off) {
-    constexpr uint32_t G = 16, BPW = 64 / G;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * BPW * SLOT];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane / G, t = lane % G;
-    uint8_t *const slot = lds + (w * BPW + q) * SLOT;
-    const uint64_t base = (uint64_t)src;
-    const uint32_t ngroups = (n + BPW - 1) / BPW;
-    for (uint32_t g = blockIdx.x * WPB + w; g < ngroups; g += gridDim.x * WPB) {
-        const uint32_t i = g * BPW + q;
-        bool act = false;
-        uint32_t status = 0, dlen = 0, clen = 0, so = 0;
-        uint64_t o0 = 0, rec = 0, rend = 0;
-        uint32_t *dw = reinterpret_cast<uint32_t *>(out + (i < n ? i : 0));
-        if (i < n) {
-            status = dw[9];
-            const uint32_t cpos = dw[2];  // provisional (header pass): value position in the record
-            if ((status == BHG_ST_OK || status == BHG_ST_CRC_MISMATCH) && cpos != 0) {
-                dlen = dw[3];
-                const bhg_handle h = handles[i];
-                clen = h.length - cpos;
-                rec = base + h.offset + cpos;
-                rend = base + h.offset + h.length;
-                o0 = val_off[i];
-                const uint64_t o1 = val_off[i + 1];
-                so = (clen + 15) & ~15u;
-                if (o1 > out_cap || o1 - o0 < dlen) {
-                    if (t == 0) {
-                        dw[2] = 0;
-                        dw[3] = 0;
-                        dw[9] = BHG_ST_SNAPPY_TOO_LARGE;
-                    }
-                } else {
-                    act = (uint64_t)so + (dlen > 16 ? dlen : 16) <= SLOT;
-                }
-            }
-        }
-        // stage the stream: 16 B per lane per step, zero past the record
-        if (act)
-            for (uint32_t off = 16 * t; off < clen; off += 16 * G)
-                *reinterpret_cast<u32x4 *>(slot + off) = ld16_hi(rec + off, rend);
-        uint32_t s = 0, d = 0;
-        bool ok = true;
-        if (act) {  // decodedLen uvarint (validated by the header pass): skip it
-            while (slot[s] >= 0x80) s++;
-            s++;
-        }
-        uint8_t *const ob = slot + so;
-        while (act) {
-            if (s >= clen) {
-                ok = d == dlen;
-                break;
-            }
-            const uint32_t a = s & ~3u, sh = s & 3u;
-            const uint32_t w0 = *reinterpret_cast<const uint32_t *>(slot + a);
-            const uint32_t w1 = *reinterpret_cast<const uint32_t *>(slot + a + 4);
-            const uint32_t w2 = *reinterpret_cast<const uint32_t *>(slot + a + 8);
-            const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            const uint32_t tag = lo & 0xffu;
-            uint32_t len, adv, off = 0;
-            bool lit = false, bad;
-            if ((tag & 3) == 0) {  // literal
-                const uint32_t x = tag >> 2;
-                uint64_t l64;
-                if (x < 60) {
-                    adv = 1;
-                    l64 = (uint64_t)x + 1;
-                    bad = false;
-                } else {
-                    const uint32_t nb = x - 59;
-                    adv = 1 + nb;
-                    const uint64_t t8 = (uint64_t)lo | ((uint64_t)hi << 32);
-                    l64 = ((t8 >> 8) & (nb >= 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
-                    bad = (uint64_t)s + adv > clen;
-                }
-                bad = bad || l64 > (uint64_t)(dlen - d) || l64 > (uint64_t)clen - s - adv;
-                len = (uint32_t)l64;
-                lit = true;
-            } else {
-                if ((tag & 3) == 1) {
-                    adv = 2;
-                    len = 4 + ((tag >> 2) & 7);
-                    off = ((tag & 0xe0u) << 3) | ((lo >> 8) & 0xffu);
-                } else if ((tag & 3) == 2) {
-                    adv = 3;
-                    len = 1 + (tag >> 2);
-                    off = (lo >> 8) & 0xffffu;
-                } else {
-                    adv = 5;
-                    len = 1 + (tag >> 2);
-                    off = (lo >> 8) | (hi << 24);
-                }
-                bad = (uint64_t)s + adv > clen || off == 0 || d < off || len > dlen - d;
-            }
-            if (bad) {
-                ok = false;
-                break;
-            }
-            const uint32_t sp = lit ? s + adv : so + d - off;  // source of element byte 0 in the slot
-            const bool wrap = !lit && off < len;
-            const float rcp = __builtin_amdgcn_rcpf((float)(off ? off : 1u));
-            for (uint32_t k0 = 0; k0 < len; k0 += G) {
-                const uint32_t k = k0 + t;
-                if (k < len) {
-                    uint32_t kk = k;
-                    if (wrap) {  // k mod off, k < 64: float quotient, one correction each way
-                        uint32_t qq = (uint32_t)((float)k * rcp);
-                        int32_t r = (int32_t)(k - qq * off);
-                        r = r < 0 ? r + (int32_t)off : r;
-                        r = r >= (int32_t)off ? r - (int32_t)off : r;
-                        kk = (uint32_t)r;
-                    }
-                    ob[d + k] = slot[sp + kk];
-                }
-            }
-            if (lit) s += len;
-            s += adv;
-            d += len;
-        }
-        if (act && ok)
-            for (uint32_t off = 16 * t; off < dlen; off += 16 * G)
-                st16_clip((uint64_t)out_vals + o0 + off, *reinterpret_cast<const u32x4 *>(ob + off),
-                          (uint64_t)out_vals + o0 + dlen);
-        if (act && t == 0) {
-            dw[2] = 0;
-            dw[3] = ok ? dlen : 0u;
-            dw[9] = ok ? status : BHG_ST_SNAPPY_CORRUPT;
-        }
-    }
-}
-
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
-    constexpr int SLOT = 3072, WPB = 4;  // 48 KiB of LDS per workgroup: three per CU
-    const uint64_t groups = (n + 3) / 4;
-    uint64_t gl = (groups + WPB - 1) / WPB;
-    const uint64_t capl = (uint64_t)L.num_cus * 3;
-    if (gl > capl) gl = capl;
-    if (gl == 0) gl = 1;
-    hipLaunchKernelGGL((k_snappy_lds<SLOT, WPB>), dim3((uint32_t)gl), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
-                       out, out_vals, out_cap, val_off);
-    // the blocks too large for a slot (their descriptors are still provisional)
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * 8;
     if (grid > cap) grid = cap;
