@@ -10,7 +10,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbithashgpu.so")
+LIB_PATH = os.environ.get("BHG_LIB_PATH") or os.path.join(_HERE, "lib", "libbithashgpu.so")  # override: lab builds
 CSRC = os.path.join(_HERE, "csrc")
 
 HANDLE_DT = np.dtype([("offset", "<u8"), ("length", "<u4"), ("pad", "<u4")])

@@ -179,12 +179,12 @@ inline void crc32c_braid_table(uint64_t fold, uint32_t *out) {
 
 // Shift tables of the tile decode kernel (bhg_decode_tile.hip), in this order:
 // Z_1024 (Horner step over 8 windows; also k_crc_long's base), Z_128, Z_256,
-// Z_512 (window distance to the record end), Z_32 (fold of the 4 interleaved
-// 32-B chains).  Device copy owned by the context.
-constexpr uint32_t kZTabWords = 5 * 1024;
+// Z_512 (window distance to the record end), Z_32 / Z_64 (fold of 4 / 2
+// interleaved window chains).  Device copy owned by the context.
+constexpr uint32_t kZTabWords = 6 * 1024;
 inline void build_tile_ztab(uint32_t *out) {
-    const uint64_t zs[5] = {1024, 128, 256, 512, 32};
-    for (uint32_t k = 0; k < 5; k++) crc32c_shift_table(zs[k], out + 1024 * k);
+    const uint64_t zs[6] = {1024, 128, 256, 512, 32, 64};
+    for (uint32_t k = 0; k < 6; k++) crc32c_shift_table(zs[k], out + 1024 * k);
 }
 
 }  // namespace bhg

@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t wave_incl_or(uint32_t x) {
 // decodedLen varint -> sizes[i]; the value is decoded by the snappy kernel).
 // KO (lab only, knock-outs for timing; outputs are then wrong): bit 0 no CRC
 // chains, 1 no scan, 2 no header loads, 3 no chain fold, 4 uniform-m locate,
-// 5 no head init / tail.
+// 5 no head init / tail, 6 no descriptor stores, 7 no shift-table loads in the prologue.
 template <int MODE, int NCH, int WPB, int WIN = 128, int PIPE = 0, int KO = 0>
 __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__restrict__ src, uint64_t src_len,
                                                             const bhg_handle *__restrict__ handles, uint32_t n,
@@ -128,10 +128,22 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
     __shared__ __attribute__((aligned(16))) uint32_t Zs[6 * 1024];
     __shared__ uint32_t E[128];
     Crc4Perm::fill(T);
-    {
-        for (uint32_t t = threadIdx.x; t < 1024; t += 64 * WPB) Zf[t] = gtab[kStreamZf + t];
-        for (uint32_t t = threadIdx.x; t < 6 * 1024; t += 64 * WPB) Zs[t] = gtab[kStreamZs + t];
-        for (uint32_t t = threadIdx.x; t < 128; t += 64 * WPB) E[t] = gtab[kStreamE + t];
+    if (!(KO & 128)) {  // all loads issued before the first LDS store (one memory round trip)
+        constexpr uint32_t NT = 64 * WPB, NZ = (7 * 1024 + NT - 1) / NT;
+        uint32_t v[NZ];
+#pragma unroll
+        for (uint32_t r = 0; r < NZ; r++) {
+            const uint32_t t = threadIdx.x + r * NT;
+            v[r] = t < 7 * 1024 ? gtab[kStreamZf + t] : 0u;  // Zf and Zs are contiguous in gtab
+        }
+        const uint32_t e = threadIdx.x < 128 ? gtab[kStreamE + threadIdx.x] : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < NZ; r++) {
+            const uint32_t t = threadIdx.x + r * NT;
+            if (t < 1024) Zf[t] = v[r];
+            else if (t < 7 * 1024) Zs[t - 1024] = v[r];
+        }
+        if (threadIdx.x < 128) E[threadIdx.x] = e;
     }
     __syncthreads();
     const Crc4Perm crc(T);
@@ -199,6 +211,15 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         // records that own windows
         auto locate = [&](uint32_t ps) {
             PassIn pi;
+            if (KO & 256) {  // probe addressing (lab): the tile's first record start + 8 KB per pass
+                const uint64_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)p) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+                pi.act = ps * 64 + lane < total;
+                pi.head = false;
+                pi.padr = 0;
+                const uint64_t a = b0 + 8192ull * ps + (uint64_t)WIN * lane, amax = end - WIN - 64;
+                pi.A = a < amax ? a : amax;  // the tile's last pass may run past the source
+                return pi;
+            }
             if (KO & 16) {  // uniform m, dense tile (lab data): r = g / m
                 const uint32_t mu = __builtin_amdgcn_readfirstlane(m);
                 const uint32_t g = ps * 64 + lane;
@@ -320,6 +341,15 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             return pi.act ? V : 0u;
         };
         auto absorb = [&](const PassIn &pi, uint32_t ps, const uint32_t (&w)[NW + 2], const uint32_t (&hwt)[16]) {
+            if (KO & 512) {  // lab: fold the words into rcrc, nothing else
+#pragma unroll
+                for (int t = 0; t < NW + 2; t++) rcrc ^= w[t];
+                if (!(KO & 4)) {
+#pragma unroll
+                    for (int t = 0; t < 16; t++) rcrc += hwt[t];
+                }
+                return;
+            }
             const uint32_t g0 = ps * 64;
             const bool hp = m != 0 && M >= g0 && M < g0 + 64;
             if (!(KO & 4)) {
@@ -347,7 +377,21 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         // PIPE: two buffers, pass ps+1 in flight while pass ps is absorbed; else one pass at a
         // time (loads of one pass never outlive its loop iteration) with more waves per CU
         auto run = [&](bool inter) {
-            if (PIPE) {
+            if (PIPE == 2) {  // software pipeline: pass ps+1's loads in flight while ps is absorbed
+                uint32_t wa[NW + 2], wb[NW + 2], ha[16], hb2[16];
+                PassIn pa = locate(0);
+                fetch(pa, 0, wa, ha, inter);
+                for (uint32_t ps = 0; ps < npass; ps++) {
+                    const PassIn pb = locate(ps + 1);  // past the last pass: every lane loads `safe`
+                    fetch(pb, ps + 1, wb, hb2, inter);
+                    absorb(pa, ps, wa, ha);
+                    pa = pb;
+#pragma unroll
+                    for (int t = 0; t < NW + 2; t++) wa[t] = wb[t];
+#pragma unroll
+                    for (int t = 0; t < 16; t++) ha[t] = hb2[t];
+                }
+            } else if (PIPE) {
                 uint32_t wa[NW + 2], wb[NW + 2], ha[16], hb[16];
                 for (uint32_t ps = 0; ps < npass; ps += 2) {
                     const PassIn pa = locate(ps);
@@ -369,6 +413,11 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         if (npass != 0) {
             if (interior) run(true);
             else run(false);
+        }
+        wait_loads_done();  // unconditional: see bhg_device.h
+        if (KO & 1024) {  // lab: no record section
+            if (rcrc == 0x9e3779b9u) out[i].crc = rcrc;
+            continue;
         }
         if (valid) {
             // ---- readRecordHeader / readRecord / readKV from the record's first 60 bytes
@@ -448,6 +497,10 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                 }
             }
             uint2 *o = reinterpret_cast<uint2 *>(out + i);
+            if (KO & 64) {
+                if (dcrc == 0x9e3779b9u) o[4] = make_uint2(dcrc, dst);
+                continue;
+            }
             o[0] = make_uint2(dk, dkl);
             o[1] = make_uint2(dvo, dvl);
             o[2] = make_uint2((uint32_t)dtr, (uint32_t)(dtr >> 32));

@@ -32,6 +32,10 @@
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
+#ifndef BHG_TILE_NCH
+#define BHG_TILE_NCH 2  // measured: 1 / 2 / 4 chains 0.2455 / 0.2413 / 0.2445 ms (scripts/lab/run_tilevar.sh)
+#endif
+
 namespace bhg {
 
 namespace {
@@ -47,17 +51,29 @@ __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
 
 }  // namespace
 
-template <int WPB>
+// NCH: interleaved CRC chains per 128-B window (1, 2 or 4), folded with Z_{128/NCH}.  With
+// 2 waves per SIMD and a round's loads in flight, one chain's 32 dependent steps hide behind
+// memory; every fold costs a conflicted shift-table lookup.
+template <int WPB, int NCH>
 __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restrict__ src, uint64_t src_len,
                                                           const bhg_handle *__restrict__ handles, uint32_t n,
                                                           const uint32_t *__restrict__ expected_crc,
                                                           bhg_desc *__restrict__ out, const uint32_t *__restrict__ gz) {
     __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Perm::kWords];
-    __shared__ __attribute__((aligned(16))) uint32_t Z[kZTabWords];  // Z1024, Z128, Z256, Z512, Z32
+    __shared__ __attribute__((aligned(16))) uint32_t Z[kZTabWords];  // Z1024, Z128, Z256, Z512, Z32, Z64
     Crc4Perm::fill(T);
-    for (uint32_t t = threadIdx.x; t < kZTabWords; t += 64 * WPB) Z[t] = gz[t];
+    {  // all loads issued before the first LDS store (one memory round trip)
+        constexpr uint32_t NT = 64 * WPB, NZ = (kZTabWords + NT - 1) / NT;
+        uint32_t v[NZ];
+#pragma unroll
+        for (uint32_t r = 0; r < NZ; r++) v[r] = threadIdx.x + r * NT < kZTabWords ? gz[threadIdx.x + r * NT] : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < NZ; r++)
+            if (threadIdx.x + r * NT < kZTabWords) Z[threadIdx.x + r * NT] = v[r];
+    }
     __syncthreads();
-    const uint32_t *Z32 = Z + 4096;
+    static_assert(NCH == 1 || NCH == 2 || NCH == 4, "chains per window");
+    const uint32_t *Zf = Z + (NCH == 4 ? 4096 : 5120);  // fold table Z_{128 / NCH}
     const Crc4Perm crc(T);
     const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
     const uint64_t base = (uint64_t)src, end = base + src_len;
@@ -77,6 +93,8 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
         }
         const bool valid = i < n;
+        // requested here, used after phase 2: a load issued at the end would expose its latency per tile
+        const uint32_t ecrc = (expected_crc != nullptr && valid) ? expected_crc[i] : 0u;
         uint32_t st = BHG_ST_OK;
         bool inb = false;
         if (valid) {
@@ -203,6 +221,9 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
                 }
             }
         }
+        // the head lane of phase 2 (j == (m-1) % 8) owns windows iff m >= 9; its first Horner step
+        // applies Z_1024 to the head CRC, done here once per record
+        const uint32_t hz = m >= 9 ? zapply(Z, hcrc) : hcrc;
         // ---------------- phase 2: 8 rounds; lane (rr, j) on record 8s + rr
 #pragma unroll
         for (uint32_t s = 0; s < 8; s++) {
@@ -215,23 +236,37 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
                 rinfo(s + 1, wb, mm, qf, q0, hasw);
                 if (hasw) load_win(fw[cb ^ 1], wb, qf);
             }
-            const uint32_t hc = __shfl(hcrc, 8 * s + rr, 64);
+            const uint32_t hc = __shfl(hz, 8 * s + rr, 64);
             uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
+            // every window of the round dword-aligned (records at 4-aligned offsets): no byte shifts
+            const bool wal = __ballot(hasw_c && (wb_c & 3) != 0) == 0;
             if (hasw_c) {
                 const uint32_t wsh = (uint32_t)(wb_c & 3);
                 for (int32_t q = qf_c;; q += 8) {
-                    uint32_t c[4] = {0, 0, 0, 0};
+                    constexpr uint32_t CW = 32 / NCH;  // words per chain
+                    uint32_t c[NCH];
 #pragma unroll
-                    for (uint32_t t = 0; t < 8; t++)
+                    for (int kk = 0; kk < NCH; kk++) c[kk] = 0;
+                    if (wal) {
 #pragma unroll
-                        for (uint32_t kk = 0; kk < 4; kk++) {
-                            const uint32_t wi = 8 * kk + t;
-                            c[kk] = crc.word(c[kk], __builtin_amdgcn_alignbyte(fw[cb][wi + 1], fw[cb][wi], wsh));
-                        }
-                    uint32_t V = zapply(Z32, c[0]) ^ c[1];
-                    V = zapply(Z32, V) ^ c[2];
-                    V = zapply(Z32, V) ^ c[3];
-                    acc = zapply(Z, acc) ^ V;
+                        for (uint32_t t = 0; t < CW; t++)
+#pragma unroll
+                            for (uint32_t kk = 0; kk < NCH; kk++) c[kk] = crc.word(c[kk], fw[cb][CW * kk + t]);
+                    } else {
+#pragma unroll
+                        for (uint32_t t = 0; t < CW; t++)
+#pragma unroll
+                            for (uint32_t kk = 0; kk < NCH; kk++) {
+                                const uint32_t wi = CW * kk + t;
+                                c[kk] = crc.word(c[kk], __builtin_amdgcn_alignbyte(fw[cb][wi + 1], fw[cb][wi], wsh));
+                            }
+                    }
+                    uint32_t V = c[0];
+#pragma unroll
+                    for (int kk = 1; kk < NCH; kk++) V = zapply(Zf, V) ^ c[kk];
+                    // Horner over this lane's windows; the first step's Z_1024 of the head CRC was
+                    // applied per record in phase 1 (hz)
+                    acc = (q == qf_c ? acc : zapply(Z, acc)) ^ V;
                     if (q + 8 > q0_c) break;
                     load_win(fw[cb], wb_c, q + 8);  // records longer than 9 windows (synchronous)
                 }
@@ -245,6 +280,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);  // record 8s + r sits on lane 8r
             if ((lane >> 3) == s) mycrc = got;
         }
+        wait_loads_done();  // unconditional: see bhg_device.h
         if (valid) {
             uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
             uint64_t dtr = 0;
@@ -253,18 +289,20 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
                 if (rvalid) {
                     dk = 12; dkl = key_len; dvo = 12 + k; dvl = v;  // noCompressor.Decode: zero-copy view
                     dtr = trailer; dfn = fn; dfnv = fnv;
-                    if (expected_crc != nullptr && expected_crc[i] != dcrc) dst = BHG_ST_CRC_MISMATCH;
+                    if (expected_crc != nullptr && ecrc != dcrc) dst = BHG_ST_CRC_MISMATCH;
                 } else {
                     dst = BHG_ST_RECORD_NIL;  // ErrBhReadRecordNil
                 }
             }
-            // measured: staging these through LDS into contiguous 16-B stores changes nothing (0.286 ms both)
-            uint2 *o = reinterpret_cast<uint2 *>(out + i);
-            o[0] = make_uint2(dk, dkl);
-            o[1] = make_uint2(dvo, dvl);
-            o[2] = make_uint2((uint32_t)dtr, (uint32_t)(dtr >> 32));
-            o[3] = make_uint2(dfn, dfnv);
-            o[4] = make_uint2(dcrc, dst);
+            // non-temporal: descriptor writes mixed into the read stream cost ~0.03 ms per 40 MB
+            // as plain stores on most boxes, ~0.013 less as nt (probe_lab tile9r_st / _st_nt);
+            // staging them through LDS into contiguous 16-B stores changes nothing
+            uint64_t *o = reinterpret_cast<uint64_t *>(out + i);
+            __builtin_nontemporal_store((uint64_t)dk | ((uint64_t)dkl << 32), o);
+            __builtin_nontemporal_store((uint64_t)dvo | ((uint64_t)dvl << 32), o + 1);
+            __builtin_nontemporal_store(dtr, o + 2);
+            __builtin_nontemporal_store((uint64_t)dfn | ((uint64_t)dfnv << 32), o + 3);
+            __builtin_nontemporal_store((uint64_t)dcrc | ((uint64_t)dst << 32), o + 4);
         }
     }
 }
@@ -277,7 +315,7 @@ hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_
     uint64_t cap = (uint64_t)L.num_cus;  // 148 KiB of LDS: one workgroup per CU
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_tile<WPB>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
+    hipLaunchKernelGGL((k_decode_tile<WPB, BHG_TILE_NCH>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
                        expected_crc, out, L.ztab);
     return hipGetLastError();
 }

@@ -35,6 +35,14 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
     *reinterpret_cast<BHG_GLOBAL T *>(a) = v;
 }
 
+// s_waitcnt vmcnt(0) as a real S_WAITCNT the compiler's wait-insertion pass
+// understands (expcnt / lgkmcnt left at their maxima; gfx9 encoding).  Placed
+// before a wave's descriptor stores at the end of a tile: every load is
+// complete there anyway, and the pass then knows nothing loaded is pending at
+// the loop latch -- otherwise it merges the back edge conservatively and waits
+// vmcnt(0) after the stores, exposing a full store round trip per tile.
+__device__ __forceinline__ void wait_loads_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ uint32_t crc_table_entry(uint32_t i) {
     uint32_t c = i;
 #pragma unroll

@@ -143,6 +143,21 @@ struct Lab {
 };
 static const Lab kLab[] = {
     {"stream_c4", L_stream<4, 8, 128, 0>, false},
+    {"stream_pipe", L_stream<4, 8, 128, 0, 1>, false},
+    {"stream_pipe2", L_stream<4, 8, 128, 0, 2>, false},
+    {"stream_w256_c4", L_stream<4, 8, 256, 0>, false},
+    {"stream_w256_c8", L_stream<8, 8, 256, 0>, false},
+    {"stream_w16", L_stream<4, 16, 128, 0>, false},
+    {"stream_w12", L_stream<4, 12, 128, 0>, false},
+    {"bis_probe", L_stream<4, 8, 128, 59 | 256 | 512 | 1024>, true},
+    {"bis_probe_desc", L_stream<4, 8, 128, 59 | 256 | 512>, true},
+    {"bis_probe_absorb", L_stream<4, 8, 128, 59 | 256 | 1024>, true},
+    {"bis_probe_locate", L_stream<4, 8, 128, 43 | 512 | 1024>, true},
+    {"bis_probe_locate_u", L_stream<4, 8, 128, 59 | 512 | 1024>, true},
+    {"bis_probe_nohdr", L_stream<4, 8, 128, 63 | 4 | 256 | 512 | 1024>, true},
+    {"ko_nodesc", L_stream<4, 8, 128, 64>, true},
+    {"ko_noztab", L_stream<4, 8, 128, 128>, true},
+    {"ko_all_nodesc", L_stream<4, 8, 128, 63 | 64 | 128>, true},
     {"ko_uniform_locate", L_stream<4, 8, 128, 16>, false},
     {"ko_noscan", L_stream<4, 8, 128, 2>, true},
     {"ko_nohdr", L_stream<4, 8, 128, 4>, true},
@@ -208,7 +223,8 @@ int main(int argc, char **argv) {
         for (uint32_t i = 0; i < n; i++) e[i] = hr[i].crc;
         CK(hipMemcpy(dexp, e.data(), n * 4, hipMemcpyHostToDevice));
     }
-    Ctx c{src, len, dh, n, out, use_exp ? dexp : nullptr, tab, sink, s, prop.multiProcessorCount};
+    const uint32_t nrun = getenv("LAB_N") ? (uint32_t)atoi(getenv("LAB_N")) : n;
+    Ctx c{src, len, dh, nrun, out, use_exp ? dexp : nullptr, tab, sink, s, prop.multiProcessorCount};
     // clocks ramp over the first ~100 launches: warm up
     const int warm = getenv("LAB_WARM") ? atoi(getenv("LAB_WARM")) : 300;
     for (int it = 0; it < warm; it++)
@@ -228,7 +244,7 @@ int main(int argc, char **argv) {
         std::vector<float> ts;
         for (int it = 0; it < iters; it++) {
             CK(hipEventRecord(a, s));
-            if (bhg_decode_batch(ctx, src, len, dh, n, 0, c.exp, ref, nullptr, 0, nullptr, s) != 0) return 1;
+            if (bhg_decode_batch(ctx, src, len, dh, nrun, 0, c.exp, ref, nullptr, 0, nullptr, s) != 0) return 1;
             CK(hipEventRecord(b, s));
             CK(hipEventSynchronize(b));
             float ms;
@@ -265,7 +281,7 @@ int main(int argc, char **argv) {
         if (!l.diag) {
             CK(hipMemcpy(ho.data(), out, n * sizeof(bhg_desc), hipMemcpyDeviceToHost));
             uint32_t bad = 0, first = ~0u;
-            for (uint32_t i = 0; i < n; i++)
+            for (uint32_t i = 0; i < nrun; i++)
                 if (memcmp(&hr[i], &ho[i], sizeof(bhg_desc)) != 0) {
                     if (first == ~0u) first = i;
                     bad++;
