@@ -157,6 +157,10 @@ def run(a, world, rank, local, dev, codec):
     def step():
         codec.decode_batch(src_t, src_t.numel(), h_t, n, expected_crc=exp_crc, out_desc=desc_t)
 
+    # the measured D2D copy ceiling of the same bytes, taken BEFORE the warm-up steps: its ~40 ms of
+    # HBM streaming also brings the MI355X clocks out of idle (they ramp over ~30 ms of load,
+    # profiles/r1_s6_clock_ramp_probe.txt), so a short --warmup times steady-state clocks
+    copy_gbps, copy_ms = copy_ceiling(src_t, dev, reps=100)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -196,7 +200,6 @@ def run(a, world, rank, local, dev, codec):
     from bitalosdb_amd import shard
     digest = shard.block_digest(d["crc"], d["fnv1"], d["trailer"], d["status"])
     elapsed, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok_blocks, n, digest, dev)
-    copy_gbps, copy_ms = copy_ceiling(src_t, dev)
 
     total_blocks = n_total * a.steps
     value = total_blocks * L / elapsed / 2 ** 30
@@ -223,11 +226,12 @@ def run(a, world, rank, local, dev, codec):
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": "not measured in this run: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of "
                                        "the same command, committed in profiles/pmc_decode_c2.json",
-                     "kernel": "k_decode_tile<8>", "kernel_avg_ms": round(avg_kern_ms, 4),
+                     "kernel": "k_decode_tile<8, 2>", "kernel_avg_ms": round(avg_kern_ms, 4),
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK + 4,
                      "measured_copy_ceiling": {"GBps": round(copy_gbps, 1), "ms": round(copy_ms, 4),
-                                               "what": "torch D2D copy of the same %d B (read + write)"
-                                                       % src_t.numel(),
+                                               "what": "torch D2D copy of the same %d B (read + write), "
+                                                       "100 reps run before the warm-up steps (they also ramp "
+                                                       "the clocks)" % src_t.numel(),
                                                "frac_of_copy": round(achieved / copy_gbps, 4)}},
         "status_ok_blocks": int(ok_total),
         "valid": bool(ok_total == n_total),

@@ -48,10 +48,6 @@ namespace {
 
 typedef u32x4 u32x4u __attribute__((aligned(1)));
 
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int srcl) {
-    const uint32_t lo = __shfl((uint32_t)v, srcl, 64), hi = __shfl((uint32_t)(v >> 32), srcl, 64);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
 typedef uint64_t u64u __attribute__((aligned(1)));
 
 __device__ __forceinline__ uint64_t ld64_bounded(uint64_t a, uint64_t hi) {
@@ -163,180 +159,7 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
     return d == dlen;
 }
 
-typedef u32x4 u32x4_lds_u __attribute__((aligned(1)));
-typedef uint64_t u64_lds_u __attribute__((aligned(1)));
-
-// The same element walk on a block staged in LDS: stream [sp, sp + slen), output [op, op + dlen),
-// both byte offsets into one LDS slot.  Sources are read 4 x 16 B before any store of the element
-// (LDS is ordered per wave, so a later read sees every earlier store); stores overshoot the
-// element's end by up to 15 B, into bytes the next elements rewrite (the output area keeps 16 B
-// of slack after dlen).
-__device__ __forceinline__ bool snappy_decode_lds(uint8_t *lds, uint32_t sp, uint32_t slen, uint32_t op,
-                                                  uint32_t dlen) {
-    uint32_t s = 0, d = 0;
-    while (s < slen) {
-        const uint64_t t8 = *reinterpret_cast<const u64_lds_u *>(lds + sp + s);  // may read past the stream: masked below
-        const uint32_t tag = (uint32_t)t8 & 0xffu;
-        uint32_t n, R, a;
-        if ((tag & 3) == 0) {  // literal
-            uint32_t x = tag >> 2;
-            uint64_t l64;
-            if (x < 60) {
-                s += 1;
-                l64 = (uint64_t)x + 1;
-            } else {
-                const uint32_t nb = x - 59;
-                if ((uint64_t)s + 1 + nb > slen) return false;
-                s += 1 + nb;
-                x = (uint32_t)(t8 >> 8) & (nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u));
-                l64 = (uint64_t)x + 1;
-            }
-            if (l64 > (uint64_t)(dlen - d) || l64 > (uint64_t)(slen - s)) return false;
-            n = (uint32_t)l64;
-            a = sp + s;
-            R = n;
-            s += n;
-        } else {
-            uint32_t offset;
-            if ((tag & 3) == 1) {
-                if ((uint64_t)s + 2 > slen) return false;
-                s += 2;
-                n = 4 + ((tag >> 2) & 7);
-                offset = ((tag & 0xe0) << 3) | ((uint32_t)(t8 >> 8) & 0xffu);
-            } else if ((tag & 3) == 2) {
-                if ((uint64_t)s + 3 > slen) return false;
-                s += 3;
-                n = 1 + (tag >> 2);
-                offset = (uint32_t)(t8 >> 8) & 0xffffu;
-            } else {
-                if ((uint64_t)s + 5 > slen) return false;
-                s += 5;
-                n = 1 + (tag >> 2);
-                offset = (uint32_t)(t8 >> 8);
-            }
-            if (offset == 0 || d < offset || n > dlen - d) return false;
-            a = op + d - offset;
-            R = offset < n ? offset : n;
-        }
-        const uint32_t o = op + d;
-        const bool lit = (tag & 3) == 0;
-        for (uint32_t k = 0; k < n;) {
-            const uint32_t seg = lit ? (n - k < 64u ? n - k : 64u) : n;  // copies are <= 64 B
-            const uint32_t src = lit ? a + k : a;
-            const uint32_t rb = lit ? seg : R;
-            const u32x4 c0 = *reinterpret_cast<const u32x4_lds_u *>(lds + src);
-            const u32x4 c1 = *reinterpret_cast<const u32x4_lds_u *>(lds + src + 16);
-            const u32x4 c2 = *reinterpret_cast<const u32x4_lds_u *>(lds + src + 32);
-            const u32x4 c3 = *reinterpret_cast<const u32x4_lds_u *>(lds + src + 48);
-            for (uint32_t t = 0; t < seg; t += rb) {
-                uint8_t *q = lds + o + k + t;
-                *reinterpret_cast<u32x4_lds_u *>(q) = c0;
-                if (rb > 16 && t + 16 < seg) *reinterpret_cast<u32x4_lds_u *>(q + 16) = c1;
-                if (rb > 32 && t + 32 < seg) *reinterpret_cast<u32x4_lds_u *>(q + 32) = c2;
-                if (rb > 48 && t + 48 < seg) *reinterpret_cast<u32x4_lds_u *>(q + 48) = c3;
-            }
-            k += seg;
-        }
-        d += n;
-    }
-    return d == dlen;
-}
-
 }  // namespace
-
-// ---------------------------------------------------------------------------
-// k_snappy_ls: lane per block, the block staged in LDS.  A wave takes BPW
-// consecutive blocks; the whole wave copies each block's stream into the
-// block's LDS slot with contiguous 16-B loads (one 1-KB request per wave
-// instruction), lane b walks block b's elements entirely in LDS (tag reads,
-// literal and copy-source reads, stores: an LDS round trip per element instead
-// of an HBM/L2 one, and no line of the stream or of the output is fetched
-// twice), then the whole wave writes each decoded block out with contiguous
-// 16-B stores.  Blocks whose stream or output exceed the slot decode in their
-// lane with snappy_decode_rt (global memory), as before.
-// Slot = SO stream bytes + OB output bytes + 16 B of store slack (+ 64 B of
-// read slack for the 4 x 16 B source reads near the slot end).
-// ---------------------------------------------------------------------------
-template <int BPW, int SO, int OB>
-__global__ __launch_bounds__(64) void k_snappy_ls(const uint8_t *__restrict__ src, uint64_t src_len,
-                                                  const bhg_handle *__restrict__ handles, uint32_t n,
-                                                  bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
-                                                  uint64_t out_cap, const uint64_t *__restrict__ val_off) {
-    constexpr uint32_t SLOT = SO + OB + 16 + 64;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint64_t oend = (uint64_t)out_vals + out_cap;
-    const uint32_t ngroups = (n + BPW - 1) / BPW;
-    for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-        const uint32_t i = g * BPW + lane;
-        // ---- per block (lane < BPW): provisional descriptor from the header pass
-        uint32_t status = BHG_ST_RECORD_NIL, cpos = 0, dlen = 0, clen = 0, fin = 0;
-        uint64_t cp = 0, o0 = 0;
-        bool act = false, staged = false;
-        if (lane < BPW && i < n) {
-            const uint32_t *dw = reinterpret_cast<const uint32_t *>(out + i);
-            status = dw[9];
-            if (status == BHG_ST_OK || status == BHG_ST_CRC_MISMATCH) {
-                cpos = dw[2];
-                dlen = dw[3];
-                const bhg_handle h = handles[i];
-                cp = base + h.offset + cpos;
-                clen = h.length - cpos;
-                o0 = val_off[i];
-                const uint64_t o1 = val_off[i + 1];
-                act = true;
-                fin = status;
-                if (o1 > out_cap || o1 - o0 < dlen) {
-                    fin = BHG_ST_SNAPPY_TOO_LARGE;
-                    act = false;
-                } else {
-                    staged = clen <= SO && dlen <= OB;
-                }
-            }
-        }
-        uint8_t *const slot = lds + (lane < BPW ? lane : 0) * SLOT;
-        // ---- stage: block b's stream [cp, cp + clen) -> slot b, 16 B per lane per instruction
-        for (uint32_t b = 0; b < BPW; b++) {
-            const uint32_t cl = __shfl(staged ? clen : 0u, (int)b, 64);
-            if (cl == 0) continue;  // wave-uniform
-            const uint64_t c = shfl_u64(cp, (int)b);
-            for (uint32_t off = 16 * lane; off < cl; off += 1024)
-                *reinterpret_cast<u32x4 *>(lds + b * SLOT + off) = ld16_hi(c + off, c + cl);
-        }
-        // ---- decode: lane b walks block b in LDS
-        if (staged) {
-            uint32_t hdr = 0;
-            while (slot[hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
-            hdr++;
-            if (!snappy_decode_lds(slot, hdr, clen - hdr, SO, dlen)) fin = BHG_ST_SNAPPY_CORRUPT;
-        } else if (act) {
-            uint32_t hdr = 0;
-            for (;;) {
-                const uint32_t bb = gld<uint8_t>(cp + hdr);
-                hdr++;
-                if (bb < 0x80) break;
-            }
-            if (!snappy_decode_rt(cp + hdr, clen - hdr, (uint64_t)out_vals + o0, dlen, end, oend))
-                fin = BHG_ST_SNAPPY_CORRUPT;
-        }
-        // ---- write out: block b's decoded bytes -> out_vals[o0, o0 + dlen), 16 B per lane per instruction
-        const bool good = staged && (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH);
-        for (uint32_t b = 0; b < BPW; b++) {
-            const uint32_t dl = __shfl(good ? dlen : 0u, (int)b, 64);
-            if (dl == 0) continue;  // wave-uniform
-            const uint64_t o = (uint64_t)out_vals + shfl_u64(o0, (int)b);
-            for (uint32_t off = 16 * lane; off < dl; off += 1024)
-                st16_clip(o + off, *reinterpret_cast<const u32x4 *>(lds + b * SLOT + SO + off), o + dl);
-        }
-        if (lane < BPW && i < n && (status == BHG_ST_OK || status == BHG_ST_CRC_MISMATCH)) {
-            uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
-            dw[2] = 0;
-            dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? dlen : 0u;
-            dw[9] = fin;
-        }
-    }
-}
 
 __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
@@ -373,24 +196,8 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
     }
 }
 
-#ifndef BHG_SNAPPY_LS
-#define BHG_SNAPPY_LS 0
-#endif
-#ifndef BHG_LS_BPW
-#define BHG_LS_BPW 32
-#endif
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
-    if (BHG_SNAPPY_LS) {
-        constexpr uint32_t BPW = BHG_LS_BPW;
-        const uint32_t groups = (n + BPW - 1) / BPW;
-        const uint32_t cap = (uint32_t)L.num_cus * 16;
-        uint32_t grid = groups < cap ? groups : cap;
-        if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_snappy_ls<BPW, 768, 1024>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                           out_vals, out_cap, val_off);
-        return hipGetLastError();
-    }
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * 8;
     if (grid > cap) grid = cap;
