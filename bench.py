@@ -225,7 +225,7 @@ def run(a, world, rank, local, dev, codec):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": "not measured in this run: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of "
-                                       "the same command, committed in profiles/pmc_decode_c2.json",
+                                       "the same command, committed in profiles/pmc_decode_c2.json (k_decode_tile<8, 2>, scripts/profile_bench.sh)",
                      "kernel": "k_decode_tile<8, 2>", "kernel_avg_ms": round(avg_kern_ms, 4),
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK + 4,
                      "measured_copy_ceiling": {"GBps": round(copy_gbps, 1), "ms": round(copy_ms, 4),
@@ -390,14 +390,21 @@ def run_c3(a, world, rank, local, dev, codec):
                       "blocks_per_gpu": n, "mean_record_bytes": round(disk / n, 1),
                       "decoded_GiBps": round(n * 1024 * a.steps / el / 2 ** 30, 3)},
            "status_ok_blocks": int((d["status"] == 0).sum())}
+    # SURVEY 8(d) C3 algorithmic bytes: handle 16 + record L + desc 40 + 1 KiB decoded value per block,
+    # over the whole step (header/CRC pass + scan + snappy kernel; kms = event-timed step)
+    alg = n * (16 + 40 + 1024) + disk
+    out["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "traffic": None, "scope": "whole step (k_decode_stream<1> + scan + k_snappy_rt)",
+                       "step_event_ms": round(kms, 4)}
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         host = src.cpu().numpy()
-        exp, ev, eo = O.decode_batch(host, h, codec=1, nthreads=min(16, os.cpu_count() or 1))
+        thr = usable_cores()
+        exp, ev, eo = O.decode_batch(host, h, codec=1, nthreads=thr)
         got_v = vals.cpu().numpy()
         par = all(np.array_equal(exp[f], d[f]) for f in d.dtype.names) and \
             got_v[:int(eo[-1])].tobytes() == ev[:int(eo[-1])].tobytes()
-        thr = min(16, os.cpu_count() or 1)
         t = time.perf_counter()
         reps = 0
         while time.perf_counter() - t < a.cpu_seconds:
@@ -405,7 +412,9 @@ def run_c3(a, world, rank, local, dev, codec):
             reps += 1
         cs = time.perf_counter() - t
         out["cpu_baseline"] = {"value": round(reps * disk / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": thr,
-                               "kind": "port", "sample": "%d passes over the same %d blocks (%s)" % (reps, n, cpu_info())}
+                               "kind": "port", "sample": "C restatement (readRecord + CRC + golang/snappy decode), "
+                               "%d passes over the same %d blocks on %d threads = every core this process may use "
+                               "(%s)" % (reps, n, thr, cpu_info())}
         out["parity_vs_restatement"] = "bit-exact" if par else "MISMATCH"
     if rank == 0:
         print(json.dumps(out), flush=True)
