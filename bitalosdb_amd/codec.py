@@ -166,15 +166,23 @@ class BithashCodec:
         self.sync()
         return res.desc_np(), None, None
 
-    def decode_host(self, src, handles, compressor=NoCompressor, expected_crc=None, out_vals_cap=None):
+    def decode_host(self, src, handles, compressor=NoCompressor, expected_crc=None, out_vals_cap=None,
+                    out_desc=None):
         """End-to-end path: host buffers in and out (bhg_decode_batch_host).
         Snappy with out_vals_cap None runs the sizing pass first (out_vals NULL)
-        and allocates exactly out_val_off[n] bytes."""
+        and allocates exactly out_val_off[n] bytes.  out_desc: an optional
+        caller-owned DESC_DT array of n entries (e.g. host_register'ed once and
+        reused: the NoCompressor path then writes it in place)."""
         src = np.ascontiguousarray(np.frombuffer(src, np.uint8) if isinstance(src, (bytes, bytearray)) else src,
                                    dtype=np.uint8)
         h = np.ascontiguousarray(handles, dtype=HANDLE_DT)
         n = len(h)
-        desc = np.zeros(n, dtype=DESC_DT)
+        if out_desc is not None:
+            if out_desc.dtype != DESC_DT or len(out_desc) < n or not out_desc.flags["C_CONTIGUOUS"]:
+                raise ValueError("out_desc must be a contiguous DESC_DT array of >= n entries")
+            desc = out_desc[:n]
+        else:
+            desc = np.empty(n, dtype=DESC_DT)
         exp = None if expected_crc is None else np.ascontiguousarray(expected_crc, dtype=np.uint32)
         off = np.zeros(n + 1, dtype=np.uint64) if compressor == SnappyCompressor else None
         cap = 0

@@ -160,16 +160,22 @@ int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const b
  * is the end-to-end path (mmap'd .bht -> H2D -> kernel -> D2H).  For codec
  * NONE with handles sorted by offset (table scans, compaction) the batch is
  * pipelined in <= 64 MiB chunks over 3 streams, so H2D, kernels and D2H
- * overlap; otherwise src is copied whole first.  SNAPPY: the device value
+ * overlap (pin src and reuse a pinned out_desc for the link rate); with
+ * unsorted handles a page-locked + mapped src (bhg_host_register,
+ * bhg_malloc_host) is decoded in place over PCIe with no staging copy
+ * (out_desc / handles / expected_crc used in place too when mapped);
+ * otherwise src is copied whole first.  SNAPPY always stages src in HBM.
+ * SNAPPY: the device value
  * buffer is sized from the scanned total (not from out_vals_cap); out_vals
  * NULL returns only out_val_off (the sizing pass). */
 int bhg_decode_batch_host(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                           uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                           uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off);
 
-/* Page-lock (pin) a caller host range, e.g. an mmap'd .bht file, so the
- * *_host paths copy it by DMA at the link rate instead of through pageable
- * staging (hipHostRegister).  Unregister before unmapping. */
+/* Page-lock (pin) a caller host range, e.g. an mmap'd .bht file, and map it
+ * into the device address space (hipHostRegister, mapped + portable): the
+ * *_host paths then read it in place (NoCompressor) or copy it by DMA at the
+ * link rate instead of through pageable staging.  Unregister before unmapping. */
 int bhg_host_register(bhg_ctx *ctx, void *p, uint64_t bytes);
 int bhg_host_unregister(bhg_ctx *ctx, void *p);
 

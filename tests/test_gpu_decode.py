@@ -454,7 +454,8 @@ def test_host_pipelined_sorted(chunk, big, monkeypatch):
 
 
 def test_host_pipelined_registered(codec):
-    """Pinned (bhg_host_register) host source through the pipelined path."""
+    """Pinned (bhg_host_register) host source: the zero-copy path (the kernel
+    reads the mapped source in place)."""
     rng = random.Random(77)
     specs = [(rand_bytes(rng, 32), rand_bytes(rng, 1024), 3) for _ in range(4000)]
     src, h = make_records(rng, specs)
@@ -466,3 +467,37 @@ def test_host_pipelined_registered(codec):
         codec.host_unregister(buf)
     exp, _, _ = O.decode_batch(src, h)
     assert_desc_equal(got, exp)
+
+
+@pytest.mark.parametrize("pin_desc", [False, True])
+def test_host_mapped_unsorted(codec, pin_desc):
+    """Zero-copy host path: page-locked + mapped source, handles in random order
+    (no pipeline needed), edge statuses, expected_crc, and a reused descriptor
+    buffer that is itself mapped (written in place) or pageable (D2H)."""
+    from bitalosdb_amd.codec import DESC_DT
+    rng = random.Random(91)
+    specs = [(rand_bytes(rng, rng.choice([0, 7, 32, 40])), rand_bytes(rng, rng.choice([1, 64, 1024, 3000])), 4)
+             for _ in range(3000)]
+    src, h = make_records(rng, specs, gap_max=3)
+    h = h.copy()
+    h["length"][10] = 0                        # ErrBhIllegalBlockLength
+    h["offset"][20] = len(src) - 5             # runs past src: INCOMPLETE
+    perm = np.random.default_rng(5).permutation(len(h))
+    h = h[perm]
+    exp0, _, _ = O.decode_batch(src, h)
+    expected = exp0["crc"].copy()
+    expected[3::89] ^= 1
+    buf = np.frombuffer(src, np.uint8).copy()
+    out = np.empty(len(h), dtype=DESC_DT)
+    codec.host_register(buf)
+    if pin_desc:
+        codec.host_register(out)
+    try:
+        got, _, _ = codec.decode_host(buf, h, expected_crc=expected, out_desc=out)
+    finally:
+        if pin_desc:
+            codec.host_unregister(out)
+        codec.host_unregister(buf)
+    exp, _, _ = O.decode_batch(src, h, expected_crc=expected)
+    assert_desc_equal(got, exp)
+    assert (got["status"] == O.CRC_MISMATCH).sum() > 0
