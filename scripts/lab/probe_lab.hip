@@ -136,6 +136,14 @@ __global__ __launch_bounds__(512) void k_probe(const uint8_t *__restrict__ src, 
                 for (int q = 0; q < 5; q++) __builtin_nontemporal_store((uint64_t)acc << 32 | q, o + q);
             }
         }
+        if (ST == 9 && ORD == 0) {  // chip-linear: 8 lanes store one 40-B descriptor each per pass (~7.6 records / 8 KB)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            if ((lane & 7) == 0) {
+                uint64_t *o = reinterpret_cast<uint64_t *>(dout + ((t * 8 + (lane >> 3)) % (1u << 20)) * 40);
+#pragma unroll
+                for (int q = 0; q < 5; q++) __builtin_nontemporal_store((uint64_t)acc << 32 | q, o + q);
+            }
+        }
         if (ORD == 0) t += W * PF;
         else if (ORD == 1 || ORD == 3) {
             if (++it_k == 9) { it_k = 0; it_tile += W; t = it_tile * 9; } else t++;
@@ -201,6 +209,8 @@ static const P kP[] = {
     {"tile9r_writer_wave", L_writer},
     {"tile9r_ntld", L<0, 0, 0, 0, 1, 3, 0, 0, 1>},
     {"tile9r_st_nt", L<0, 0, 0, 0, 1, 3, 6>},
+    {"linear_st_nt", L<0, 0, 0, 0, 1, 0, 9>},
+    {"linear_crc_x8_hdr_st_nt", L<52, 1, 1, 1, 1, 0, 9>},
     {"tile9r_st_coal_nt", L<0, 0, 0, 0, 1, 3, 8>},
     {"tile9r_ntld_st_nt", L<0, 0, 0, 0, 1, 3, 6, 0, 1>},
     {"tile9r_ntld_st_coal_nt", L<0, 0, 0, 0, 1, 3, 8, 0, 1>},
