@@ -39,6 +39,9 @@ ALGO_BYTES_PER_BLOCK = 16 + 1076 + 40   # handle + record + descriptor (SURVEY Â
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (= RCCL, the real run) or gloo (rehearsal of the multi-rank "
+                         "path with several ranks on one GPU; device = LOCAL_RANK mod visible GPUs)")
     ap.add_argument("--steps", type=int, default=20)
     # GPU clocks ramp over the first ~100 C2 launches (~30 ms of load; profiles/r1_s6_clock_ramp_probe.txt)
     ap.add_argument("--warmup", type=int, default=100)
@@ -104,15 +107,47 @@ def pmc_traffic():
         return None
 
 
+BACKEND = "nccl"
+
+
+def dist_barrier(world, local):
+    """Barrier of the N>1 bench (nccl: on the rank's device stream; gloo: host)."""
+    if world > 1:
+        import torch.distributed as dist
+        if BACKEND == "nccl":
+            dist.barrier(device_ids=[local])
+        else:
+            dist.barrier()
+
+
+def dist_sum_(t, world):
+    """In-place SUM all-reduce of a small tensor (gloo: through host memory)."""
+    if world > 1:
+        import torch.distributed as dist
+        if BACKEND == "nccl":
+            dist.all_reduce(t)
+        else:
+            h = t.cpu()
+            dist.all_reduce(h)
+            t.copy_(h)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch.distributed as dist
+    global BACKEND
+    BACKEND = a.backend
+    if a.backend == "gloo":   # rehearsal: ranks may share a GPU
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -166,8 +201,7 @@ def run(a, world, rank, local, dev, codec):
     torch.cuda.synchronize(dev)
 
     def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[local])
+        dist_barrier(world, local)
 
     # timed region: K back-to-back steps, no per-step event markers in the stream
     barrier()
@@ -451,6 +485,14 @@ def run_c4(a, world, rank, local, dev, codec):
            "config": {"workload": "BASELINE configs[3]: 1M KV pairs -> record-pack + compress + CRC",
                       "pairs_per_gpu": n, "input_bytes": int(raw), "output_bytes": total,
                       "tables": int(bufs.summary[1].item())}}
+    # SURVEY 8(d) C4 algorithmic bytes: read key 32 + value v + 16 B (offsets, trailer); write the
+    # records (52 + c each, = output_bytes) + handle 8 + FNV 4 + CRC 4; whole step (kms = event-timed)
+    alg = raw + 16.0 * n + total + 16.0 * n
+    res["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                       "scope": "whole step (sizes, scan, k_snappy_enc, split, pack, crc)",
+                       "step_event_ms": round(kms, 4),
+                       "note": "k_snappy_enc is latency bound (DESIGN.md 4.3); snappy scratch traffic excluded"}
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         # bounded sample: the first 20k pairs, single thread (the restated writer is serial)
@@ -555,8 +597,7 @@ def run_c5(a, world, rank, local, dev, codec):
     torch.cuda.synchronize(dev)
 
     def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[local])
+        dist_barrier(world, local)
 
     barrier()
     torch.cuda.synchronize(dev)
@@ -579,8 +620,7 @@ def run_c5(a, world, rank, local, dev, codec):
     digest = shard.block_digest(d["crc"], d["fnv1"], d["trailer"], d["status"])
     el_max, ok_total, n_total, digest_all = shard.reduce_stats(elapsed, ok, n, digest, dev)
     dt = torch.tensor([disk, raw], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt)
+    dist_sum_(dt, world)
     disk_total, raw_total = float(dt[0].item()), float(dt[1].item())
     value = disk_total * a.steps / el_max / 2 ** 30
     # per-GPU roofline of this rank's step: algorithmic bytes (handle + record + descriptor + expected CRC,
@@ -783,8 +823,7 @@ def run_get(a, world, rank, local, dev, codec):
     e0 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     e1 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     e2 = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier(device_ids=[local])
+    dist_barrier(world, local)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
@@ -792,8 +831,7 @@ def run_get(a, world, rank, local, dev, codec):
         step(e1[i])
         e2[i].record()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier(device_ids=[local])
+    dist_barrier(world, local)
     elapsed = time.perf_counter() - t0
     get_ms = float(np.mean([x.elapsed_time(y) for x, y in zip(e0, e1)]))
     dec_ms = float(np.mean([x.elapsed_time(y) for x, y in zip(e1, e2)]))

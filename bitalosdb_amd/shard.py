@@ -42,9 +42,12 @@ def block_digest(crc, fnv1, trailer, status):
 def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
     """MAX of elapsed, SUM of block counts, per-rank digests added as two 32-bit
     lanes mod 2^32 (block_digest); returns python values.  Runs outside the timed region."""
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if multi and dist.get_backend() == "gloo":
+        device = "cpu"   # gloo reduces host tensors
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
     c = torch.tensor([ok_blocks, n_blocks, digest & 0xFFFFFFFF, digest >> 32], dtype=torch.int64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
     c = c.cpu().tolist()
