@@ -47,6 +47,7 @@ __global__ __launch_bounds__(512) void k_probe(const uint8_t *__restrict__ src, 
     uint64_t it_tile = (ORD == 1 || ORD == 3) ? w0 : blockIdx.x, it_k = 0;
     const uint32_t wv = threadIdx.x >> 6;
     const uint64_t ntile3 = (len - 80000) / 68864;
+    uint32_t ntiles_done = 0;
     for (uint64_t t = ORD == 0 ? w0 : (ORD == 1 || ORD == 3 ? w0 * 9 : blockIdx.x * 72 + wv);;) {
         if (ORD == 0 && t >= np) break;
         if ((ORD == 1 || ORD == 2) && it_tile >= ntile) break;
@@ -57,10 +58,12 @@ __global__ __launch_bounds__(512) void k_probe(const uint8_t *__restrict__ src, 
         for (int f = 0; f < PF; f++) {
             const uint64_t tt = ORD == 0 ? (t + f * W < np ? t + f * W : t) : t;
             uint64_t a = ORD == 3 ? base + it_tile * 68864 + it_k * 8192 + 128 * lane : base + tt * 8192 + 128 * lane;
+            const uint64_t arow = (ORD == 3 ? base + it_tile * 68864 + it_k * 8192 : base + tt * 8192) + 16 * lane;
             if (BP) a = (uint64_t)__shfl((int64_t)a, (int)((lane + 1) & 63), 64) - 128 * ((lane + 1) & 63) + 128 * lane;  // LDS round trip before issue
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                const u32x4 x = NTL ? __builtin_nontemporal_load(reinterpret_cast<const BHG_GLOBAL u32x4 *>(a + 16 * q)) : gld<u32x4_a4>(a + 16 * q);
+                const uint64_t la = (NTL & 2) ? arow + 1024 * q : a + 16 * q;
+                const u32x4 x = (NTL & 1) ? __builtin_nontemporal_load(reinterpret_cast<const BHG_GLOBAL u32x4 *>(la)) : gld<u32x4_a4>(la);
                 w[f][4 * q] = x.x; w[f][4 * q + 1] = x.y; w[f][4 * q + 2] = x.z; w[f][4 * q + 3] = x.w;
             }
             if (X8) {
@@ -144,11 +147,19 @@ __global__ __launch_bounds__(512) void k_probe(const uint8_t *__restrict__ src, 
                 for (int q = 0; q < 5; q++) __builtin_nontemporal_store((uint64_t)acc << 32 | q, o + q);
             }
         }
+        if (ST == 10 && ORD == 3 && it_k == 8) ntiles_done++;
         if (ORD == 0) t += W * PF;
         else if (ORD == 1 || ORD == 3) {
             if (++it_k == 9) { it_k = 0; it_tile += W; t = it_tile * 9; } else t++;
         } else {
             if (++it_k == 9) { it_k = 0; it_tile += gridDim.x; t = it_tile * 72 + wv; } else t += 8;
+        }
+    }
+    if (ST == 10) {  // all of this wave's descriptors in one burst at the end
+        for (uint32_t k = 0; k < ntiles_done; k++) {
+            uint64_t *o = reinterpret_cast<uint64_t *>(dout + (((uint64_t)(w0 + (uint64_t)k * W)) * 64 + lane) * 40);
+#pragma unroll
+            for (int q = 0; q < 5; q++) __builtin_nontemporal_store((uint64_t)acc << 32 | q, o + q);
         }
     }
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
@@ -193,6 +204,47 @@ __global__ __launch_bounds__(576) void k_probe_writer(const uint8_t *__restrict_
 static void L_writer(const uint8_t *src, uint64_t len, uint32_t *sink, int cus, hipStream_t s) {
     hipLaunchKernelGGL(k_probe_writer, dim3(cus), dim3(576), 0, s, src, len, sink, g_dout);
 }
+
+// tile-kernel phase-2 load shapes (8 records x 8 lanes per round, 8 rounds per 64-record tile, 1076-B
+// records, window region = record + 52 .. + 1076): GRP 0 = today's lane-own-window (lane (g, j) reads
+// its window 8 - j as 8 x 16 B), GRP 1 = column chunks (instruction k: lane (g, j) reads chunk j of window k,
+// 128 contiguous bytes per group per instruction); NT: non-temporal loads; ST: 40-B descriptor per lane-record
+template <int GRP, int NT, int ST>
+__global__ __launch_bounds__(512) void k_probe_round(const uint8_t *__restrict__ src, uint64_t len, uint32_t *sink,
+                                                     uint8_t *dout) {
+    __shared__ uint32_t T[32768 + 6000];
+    T[threadIdx.x] = threadIdx.x;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+    const uint64_t base = (uint64_t)src;
+    const uint64_t W = (uint64_t)gridDim.x * 8, w0 = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const uint64_t ntile = (len - 80000) / 68864;
+    uint32_t acc = T[(threadIdx.x * 7) & 1023];
+    for (uint64_t tile = w0; tile < ntile; tile += W) {
+        for (uint32_t s = 0; s < 8; s++) {
+            const uint64_t region = base + tile * 68864 + (uint64_t)(8 * s + g) * 1076 + 52;
+            u32x4 x[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint64_t a = GRP ? region + 128 * k + 16 * j : region + 128 * (7 - j) + 16 * k;
+                x[k] = NT ? __builtin_nontemporal_load(reinterpret_cast<const BHG_GLOBAL u32x4 *>(a)) : gld<u32x4_a4>(a);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc ^= x[k].x ^ x[k].y ^ x[k].z ^ x[k].w;
+        }
+        if (ST) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            uint64_t *o = reinterpret_cast<uint64_t *>(dout + ((tile * 64 + lane) % (1u << 20)) * 40);
+#pragma unroll
+            for (int q = 0; q < 5; q++) __builtin_nontemporal_store((uint64_t)acc << 32 | q, o + q);
+        }
+    }
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+template <int GRP, int NT, int ST>
+static void LR(const uint8_t *src, uint64_t len, uint32_t *sink, int cus, hipStream_t s) {
+    hipLaunchKernelGGL((k_probe_round<GRP, NT, ST>), dim3(cus), dim3(512), 0, s, src, len, sink, g_dout);
+}
 typedef void (*fn_t)(const uint8_t *, uint64_t, uint32_t *, int, hipStream_t);
 struct P {
     const char *name;
@@ -210,6 +262,21 @@ static const P kP[] = {
     {"tile9r_ntld", L<0, 0, 0, 0, 1, 3, 0, 0, 1>},
     {"tile9r_st_nt", L<0, 0, 0, 0, 1, 3, 6>},
     {"linear_st_nt", L<0, 0, 0, 0, 1, 0, 9>},
+    {"tile9r_st_burst", L<0, 0, 0, 0, 1, 3, 10>},
+    {"round_own", LR<0, 0, 0>},
+    {"round_col", LR<1, 0, 0>},
+    {"round_col_nt", LR<1, 1, 0>},
+    {"round_own_st", LR<0, 0, 1>},
+    {"round_col_st", LR<1, 0, 1>},
+    {"round_col_nt_st", LR<1, 1, 1>},
+    {"tile9r_coal", L<0, 0, 0, 0, 1, 3, 0, 0, 2>},
+    {"tile9r_coal_nt", L<0, 0, 0, 0, 1, 3, 0, 0, 3>},
+    {"tile9r_coal_st_nt", L<0, 0, 0, 0, 1, 3, 6, 0, 2>},
+    {"tile9r_coalnt_st_nt", L<0, 0, 0, 0, 1, 3, 6, 0, 3>},
+    {"tile9r_coalnt_st", L<0, 0, 0, 0, 1, 3, 1, 0, 3>},
+    {"tile9r_coalnt_crc_hdr_st_nt", L<0, 1, 0, 1, 1, 3, 6, 0, 3>},
+    {"tile9r_coal_crc_hdr_st_nt", L<0, 1, 0, 1, 1, 3, 6, 0, 2>},
+    {"tile9r_crc_x8_hdr_st_burst", L<4, 1, 1, 1, 1, 3, 10>},
     {"linear_crc_x8_hdr_st_nt", L<52, 1, 1, 1, 1, 0, 9>},
     {"tile9r_st_coal_nt", L<0, 0, 0, 0, 1, 3, 8>},
     {"tile9r_ntld_st_nt", L<0, 0, 0, 0, 1, 3, 6, 0, 1>},
