@@ -196,8 +196,275 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_snappy_lds: lane per block, the block staged in LDS, a branch-free element
+// step, and the next group's streams prefetched into registers while this
+// group decodes.
+//
+// A workgroup is one wave and owns BPW LDS slots; slot b holds block b's
+// stream [0, SO) and its output [SO + 64, SO + 64 + OB), each followed by 64 B
+// of pad.  Per group of BPW consecutive blocks:
+//   1. the group's streams (prefetched into VGPRs, one 16-B chunk per lane per
+//      block) are written into the slots;
+//   2. the NEXT group's streams are requested (loads in flight during 3-5),
+//      and the descriptors of the group after it;
+//   3. lane b walks block b entirely in LDS;
+//   4. the wave stores each decoded block with contiguous 16-B stores;
+//   5. the descriptors are finalised.
+// The element step moves every element as "ops" of 64 B: 4 x 16-B reads from
+// the source, 4 x 16-B writes to the destination, no masking.
+//   literal:         op j reads stream + s + 64 j, writes out + d + 64 j
+//   copy, offset o:  op t reads out + d - o (the same 64 B every time),
+//                    writes out + d + t * min(o, n)
+// A write past the element's end lands in bytes later elements (or the pad)
+// own and is overwritten by them in program order; for an overlapping copy
+// (o < n) the last write to every byte of the element comes from the op whose
+// period contains it and reads only bytes below d or already final (LDS is in
+// order per wave, so a read sees every earlier write of its lane).  So every
+// byte of [0, dlen) ends up right, and a typical element is one op: one LDS
+// round trip, with the next tag's read in flight alongside it.
+// Checks are the reference decoder's, as in snappy_decode_rt.  Blocks whose
+// stream or output exceed the slot decode in their lane from global memory
+// (snappy_decode_rt).
+// ---------------------------------------------------------------------------
+#ifndef BHG_SNAPPY_LDS
+#define BHG_SNAPPY_LDS 1
+#endif
+#ifndef BHG_SL_BPW
+#define BHG_SL_BPW 20
+#endif
+#ifndef BHG_SL_SO
+#define BHG_SL_SO 768
+#endif
+
+// Every LDS access of k_snappy_lds goes through these may_alias types: the slot
+// is written as 16-B chunks and read as bytes, 8-B tags and 16-B chunks, and
+// type-based alias analysis must not reorder those accesses.
+typedef uint64_t u64_lds_u __attribute__((aligned(1), may_alias));
+typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));
+
+namespace {
+
+// Lanes of the wave hand LDS bytes to each other (staging -> walk -> store-out
+// -> next staging): LDS runs a wave's accesses in program order, but the
+// compiler sees one thread and could move a read above another lane's write,
+// so each hand-over is a wavefront-scope fence.
+__device__ __forceinline__ void sl_wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// mode of a block in k_snappy_lds
+enum : uint32_t { SL_SKIP = 0, SL_LDS = 1, SL_GLOBAL = 2, SL_TOOLARGE = 3 };
+
+struct SlInfo {
+    uint64_t cp, o0;  // stream (absolute, varint header included), output offset in out_vals
+    uint32_t clen, dlen, status, mode;
+};
+
+// All loads first and unconditional (index clamped to n - 1), so the caller can
+// issue them ahead of the stream prefetch and wait for them alone (vmcnt is in
+// order: a wait for a load issued after the prefetch would wait for it too).
+template <int SO, int OB>
+__device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
+                                          const uint64_t *val_off, uint64_t base, uint64_t out_cap) {
+    const uint32_t ii = i < n ? i : n - 1;
+    const uint32_t *dw = reinterpret_cast<const uint32_t *>(out + ii);
+    const uint32_t st = dw[9];
+    const uint32_t cpos = dw[2], dlen = dw[3];  // provisional (header pass): value position in the record, decoded length
+    const bhg_handle h = handles[ii];
+    const uint64_t o0 = val_off[ii], o1 = val_off[ii + 1];
+    SlInfo r;
+    r.cp = base + h.offset + cpos;
+    r.o0 = o0;
+    r.clen = h.length - cpos;
+    r.dlen = dlen;
+    r.status = st;
+    if (i >= n || (st != BHG_ST_OK && st != BHG_ST_CRC_MISMATCH))
+        r.mode = SL_SKIP;
+    else if (o1 > out_cap || o1 - o0 < dlen)
+        r.mode = SL_TOOLARGE;
+    else
+        r.mode = (r.clen <= (uint32_t)SO && dlen <= (uint32_t)OB) ? SL_LDS : SL_GLOBAL;
+    return r;
+}
+
+// block staged at lds[sp - hdr ...]: tag stream [sp, se), output at op (all LDS byte addresses)
+__device__ __forceinline__ bool snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op, uint32_t dlen) {
+    uint32_t s = sp, d = 0;
+    bool ok = true;
+    uint64_t t8 = s < se ? *reinterpret_cast<const u64_lds_u *>(lds + s) : 0;
+    while (s < se) {
+        const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
+        const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
+        const bool lit = ty == 0;
+        const uint32_t nb = (lit && x >= 60u) ? x - 59u : 0u;  // length bytes of a long literal
+        const uint32_t lmask = nb >= 4u ? 0xffffffffu : ((1u << ((8u * nb) & 31u)) - 1u);
+        const uint64_t l64 = lit ? (nb ? (uint64_t)(b14 & lmask) + 1u : (uint64_t)x + 1u)
+                                 : (uint64_t)(ty == 1u ? 4u + (x & 7u) : 1u + x);
+        const uint32_t adv = lit ? 1u + nb : (ty == 1u ? 2u : ty == 2u ? 3u : 5u);
+        const uint32_t off = ty == 1u ? (((tag & 0xe0u) << 3) | (b14 & 0xffu)) : ty == 2u ? (b14 & 0xffffu) : b14;
+        const uint32_t rem = se - s;  // >= 1
+        const bool bad = adv > rem || l64 > (uint64_t)(dlen - d) ||
+                         (lit ? l64 > (uint64_t)(rem - adv) : (off == 0u || off > d));
+        if (bad) {
+            ok = false;
+            break;
+        }
+        const uint32_t n = (uint32_t)l64;
+        const uint32_t sn = s + adv + (lit ? n : 0u);
+        const uint64_t t8n = sn < se ? *reinterpret_cast<const u64_lds_u *>(lds + sn) : 0;  // next tag, in flight
+        const uint32_t a = lit ? s + adv : op + d - off;
+        const uint32_t o = op + d;
+        const uint32_t sstep = lit ? 64u : 0u;
+        const uint32_t dstep = lit ? 64u : (off < n ? off : n);
+        for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep) {
+            const u32x4 c0 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
+            const u32x4 c1 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 16);
+            const u32x4 c2 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 32);
+            const u32x4 c3 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 48);
+            *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = c0;
+            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 16) = c1;
+            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 32) = c2;
+            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 48) = c3;
+        }
+        d += n;
+        s = sn;
+        t8 = t8n;
+    }
+    return ok && d == dlen;
+}
+
+}  // namespace
+
+template <int BPW, int SO, int OB>
+__global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                   const bhg_handle *__restrict__ handles, uint32_t n,
+                                                   bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
+                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off) {
+    static_assert(SO % 16 == 0 && OB % 16 == 0 && SO <= 1024 && OB <= 1024, "one 16-B chunk per lane per block");
+    constexpr uint32_t OUT = SO + 64, SLOT = SO + OB + 128;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint64_t oend = (uint64_t)out_vals + out_cap;
+    const uint32_t ngroups = (n + BPW - 1) / BPW;
+    const uint32_t G = gridDim.x;
+    uint32_t g = blockIdx.x;
+    if (g >= ngroups) return;
+    auto info = [&](uint32_t grp) -> SlInfo {
+        const uint32_t i = grp * BPW + lane;
+        SlInfo r = sl_info<SO, OB>(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, base, out_cap);
+        return r;
+    };
+    u32x4 v[BPW];
+    // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
+    // past the stream load src + 0; the dump drops them) and clamped to end
+    // src (a chunk that would cross the end is loaded from end - 16 and
+    // shifted into place at the dump), so no branch and no wait is tied to the
+    // loads until the next dump.  (The launcher sends src_len < 64 elsewhere.)
+    auto chunk_addr = [&](const SlInfo &I, int b, uint32_t &clb) -> uint64_t {
+        clb = __builtin_amdgcn_readlane(I.mode == SL_LDS ? I.clen : 0u, b);
+        const uint64_t cpb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)I.cp, b) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(I.cp >> 32), b) << 32);
+        return 16 * lane < clb ? cpb + 16 * lane : base;
+    };
+    auto prefetch = [&](const SlInfo &I) {
+#pragma unroll
+        for (int b = 0; b < BPW; b++) {
+            uint32_t clb;
+            const uint64_t a = chunk_addr(I, b, clb);
+            v[b] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
+        }
+    };
+    SlInfo cur = info(g);
+    prefetch(cur);
+    SlInfo nxt = info(g + G);
+    for (; g < ngroups; g += G) {
+        // 1. this group's streams -> slots
+#pragma unroll
+        for (int b = 0; b < BPW; b++) {
+            uint32_t clb;
+            const uint64_t a = chunk_addr(cur, b, clb);
+            u32x4 c = v[b];
+            if (a + 16 > end) {  // the chunk was loaded from end - 16: its bytes start at a - (end - 16)
+                const uint32_t sh = (uint32_t)(a - (end - 16));
+                unsigned __int128 x = (unsigned __int128)c.x | ((unsigned __int128)c.y << 32) |
+                                      ((unsigned __int128)c.z << 64) | ((unsigned __int128)c.w << 96);
+                x >>= 8 * sh;
+                c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+            }
+            if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + 16 * lane) = c;
+        }
+        sl_wsync();
+        // 2. descriptors of the group after next, then the next group's streams in flight
+        const SlInfo nn = info(g + 2 * G);
+        prefetch(nxt);
+        // 3. decode
+        uint32_t fin = cur.status;
+        if (cur.mode == SL_LDS) {
+            uint8_t *const slot = lds + lane * SLOT;
+            uint32_t hdr = 0;
+            while (hdr < 5 && slot[hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
+            hdr++;
+            const uint32_t sb = lane * SLOT;
+            if (!snappy_walk_lds(lds, sb + hdr, sb + cur.clen, sb + OUT, cur.dlen)) fin = BHG_ST_SNAPPY_CORRUPT;
+        } else if (cur.mode == SL_GLOBAL) {
+            uint32_t hdr = 0;
+            for (;;) {
+                const uint32_t bb = gld<uint8_t>(cur.cp + hdr);
+                hdr++;
+                if (bb < 0x80) break;
+            }
+            if (!snappy_decode_rt(cur.cp + hdr, cur.clen - hdr, (uint64_t)out_vals + cur.o0, cur.dlen, end, oend))
+                fin = BHG_ST_SNAPPY_CORRUPT;
+        } else if (cur.mode == SL_TOOLARGE) {
+            fin = BHG_ST_SNAPPY_TOO_LARGE;
+        }
+        // 4. decoded blocks -> out_vals
+        sl_wsync();
+        {
+            const bool good = cur.mode == SL_LDS && (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH);
+            const uint32_t dl = good ? cur.dlen : 0u;
+#pragma unroll
+            for (int b = 0; b < BPW; b++) {
+                const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
+                if (16 * lane < dlb) {
+                    const uint64_t ob = (uint64_t)out_vals +
+                                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)cur.o0, b) |
+                                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(cur.o0 >> 32), b) << 32));
+                    st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + OUT + 16 * lane),
+                              ob + dlb);
+                }
+            }
+        }
+        sl_wsync();
+        // 5. descriptors
+        if (cur.mode != SL_SKIP) {
+            uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
+            dw[2] = 0;
+            dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? cur.dlen : 0u;
+            dw[9] = fin;
+        }
+        cur = nxt;
+        nxt = nn;
+    }
+}
+
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
+    if (BHG_SNAPPY_LDS && src_len >= 64) {
+        constexpr uint32_t BPW = BHG_SL_BPW, SO = BHG_SL_SO, OB = 1024;
+        constexpr uint32_t lds_bytes = BPW * (SO + OB + 128);
+        const uint32_t per_cu = (160u * 1024u) / lds_bytes;
+        const uint32_t groups = (n + BPW - 1) / BPW;
+        const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
+        uint32_t grid = groups < cap ? groups : cap;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL((k_snappy_lds<BPW, SO, OB>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+                           out_vals, out_cap, val_off);
+        return hipGetLastError();
+    }
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * 8;
     if (grid > cap) grid = cap;

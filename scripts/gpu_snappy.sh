@@ -1,13 +1,16 @@
 #!/bin/bash
-# snappy decode variants: parity tests, then C3 bench per variant
+# snappy decode: parity tests on the product library, then the C3 bench for the
+# product library and each lab variant library (scripts/lab/libvar/<name>)
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-snap}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_decode.py -k "snappy" -x -v --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_golden.py -m gpu -k "snappy or c3 or golden" -x -v --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
 tail -2 $O/pytest.txt
-for v in ${VARIANTS:-2 3}; do
-  BHG_SNAPPY_VARIANT=$v timeout -k 10 240 python -u bench.py --config c3 --no-cpu --no-e2e > $O/c3_v$v.json 2> $O/c3_v$v.err || { tail -5 $O/c3_v$v.err; exit 1; }
-  echo "v$v: $(cut -c1-400 $O/c3_v$v.json)"
+timeout -k 10 240 python -u bench.py --config c3 --no-cpu --no-e2e > $O/c3_prod.json 2> $O/c3_prod.err || { tail -5 $O/c3_prod.err; exit 1; }
+echo "prod: $(cut -c1-300 $O/c3_prod.json)"
+for v in ${VARIANTS:-}; do
+  BHG_LIB_PATH=$PWD/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 240 python -u bench.py --config c3 --no-cpu --no-e2e > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 1; }
+  echo "$v: $(cut -c1-300 $O/c3_$v.json)"
 done
