@@ -172,6 +172,7 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
         const uint32_t status = dw[9];
         if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
         const uint32_t cpos = dw[2], dlen = dw[3];  // provisional: value position in the record, decoded length
+        if (cpos == 0) continue;  // finalised by k_snappy_lds (a provisional value position is >= 12)
         const bhg_handle h = handles[i];
         const uint64_t rec = base + h.offset;
         const uint32_t clen = h.length - cpos;
@@ -201,9 +202,15 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // step, and the next group's streams prefetched into registers while this
 // group decodes.
 //
-// A workgroup is one wave and owns BPW LDS slots; slot b holds block b's
-// stream [0, SO) and its output [SO + 64, SO + 64 + OB), each followed by 64 B
-// of pad.  Per group of BPW consecutive blocks:
+// A workgroup is one wave and owns BPW LDS slots of SLOT bytes.  The block
+// decodes IN PLACE: its output grows from the slot start, its stream is staged
+// at the slot end (P = (SLOT - 8 - round16(clen)) & ~15), and the walk checks
+// before every element that its writes (which overshoot by up to 63 B) stay
+// below the next unread tag; a block that would break that (or does not fit)
+// is left for the lane-per-block k_snappy_rt pass from global memory.  At C3
+// (1 KiB values, streams <= 721 B) a 1,152-B slot never falls back, so 140
+// blocks are resident per CU instead of 80 with separate stream and output
+// areas.  Per group of BPW consecutive blocks:
 //   1. the group's streams (prefetched into VGPRs, one 16-B chunk per lane per
 //      block) are written into the slots;
 //   2. the NEXT group's streams are requested (loads in flight during 3-5),
@@ -223,18 +230,16 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // order per wave, so a read sees every earlier write of its lane).  So every
 // byte of [0, dlen) ends up right, and a typical element is one op: one LDS
 // round trip, with the next tag's read in flight alongside it.
-// Checks are the reference decoder's, as in snappy_decode_rt.  Blocks whose
-// stream or output exceed the slot decode in their lane from global memory
-// (snappy_decode_rt).
+// Checks are the reference decoder's, as in snappy_decode_rt.
 // ---------------------------------------------------------------------------
 #ifndef BHG_SNAPPY_LDS
 #define BHG_SNAPPY_LDS 1
 #endif
 #ifndef BHG_SL_BPW
-#define BHG_SL_BPW 20
+#define BHG_SL_BPW 17
 #endif
-#ifndef BHG_SL_SO
-#define BHG_SL_SO 768
+#ifndef BHG_SL_SLOT
+#define BHG_SL_SLOT 1152
 #endif
 
 // Every LDS access of k_snappy_lds goes through these may_alias types: the slot
@@ -262,10 +267,17 @@ struct SlInfo {
     uint32_t clen, dlen, status, mode;
 };
 
+// in-place slot: where a stream of clen bytes is staged (16-B aligned, 8 B of
+// tag over-read room after it)
+template <int SLOT>
+__device__ __forceinline__ uint32_t sl_pos(uint32_t clen) {
+    return ((uint32_t)SLOT - 8u - ((clen + 15u) & ~15u)) & ~15u;
+}
+
 // All loads first and unconditional (index clamped to n - 1), so the caller can
 // issue them ahead of the stream prefetch and wait for them alone (vmcnt is in
 // order: a wait for a load issued after the prefetch would wait for it too).
-template <int SO, int OB>
+template <int SLOT>
 __device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
                                           const uint64_t *val_off, uint64_t base, uint64_t out_cap) {
     const uint32_t ii = i < n ? i : n - 1;
@@ -285,39 +297,50 @@ __device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc
     else if (o1 > out_cap || o1 - o0 < dlen)
         r.mode = SL_TOOLARGE;
     else
-        r.mode = (r.clen <= (uint32_t)SO && dlen <= (uint32_t)OB) ? SL_LDS : SL_GLOBAL;
+        r.mode = (dlen <= 1024u && r.clen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
     return r;
 }
 
-// block staged at lds[sp - hdr ...]: tag stream [sp, se), output at op (all LDS byte addresses)
-__device__ __forceinline__ bool snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op, uint32_t dlen) {
-    uint32_t s = sp, d = 0;
-    bool ok = true;
-    uint64_t t8 = s < se ? *reinterpret_cast<const u64_lds_u *>(lds + s) : 0;
+// block staged in LDS: tag stream [sp, se), output at op (LDS byte addresses,
+// op < sp: in place).  Returns 0 (ok), 1 (snappy.ErrCorrupt) or 2 (an element
+// would write into the unread stream: decode the block from global memory).
+// The element decode is straight-line (selects, non-short-circuit checks) so
+// the 64 lanes of a wave do not split into per-tag-type paths; the tag read is
+// unconditional (a read at se lies inside the slot).
+__device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op,
+                                                    uint32_t dlen) {
+    uint32_t s = sp, d = 0, res = 0;
+    uint64_t t8 = *reinterpret_cast<const u64_lds_u *>(lds + s);
     while (s < se) {
         const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
         const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
-        const bool lit = ty == 0;
-        const uint32_t nb = (lit && x >= 60u) ? x - 59u : 0u;  // length bytes of a long literal
-        const uint32_t lmask = nb >= 4u ? 0xffffffffu : ((1u << ((8u * nb) & 31u)) - 1u);
-        const uint64_t l64 = lit ? (nb ? (uint64_t)(b14 & lmask) + 1u : (uint64_t)x + 1u)
-                                 : (uint64_t)(ty == 1u ? 4u + (x & 7u) : 1u + x);
-        const uint32_t adv = lit ? 1u + nb : (ty == 1u ? 2u : ty == 2u ? 3u : 5u);
-        const uint32_t off = ty == 1u ? (((tag & 0xe0u) << 3) | (b14 & 0xffu)) : ty == 2u ? (b14 & 0xffffu) : b14;
+        // all-ones masks instead of ?: so the compiler keeps this straight-line
+        const uint32_t mlit = 0u - (uint32_t)(ty == 0u), m1 = 0u - (uint32_t)(ty == 1u),
+                       m2 = 0u - (uint32_t)(ty == 2u);
+        const uint32_t mlong = mlit & (0u - (uint32_t)(x >= 60u));
+        const uint32_t nb = (x - 59u) & mlong;  // length bytes of a long literal (1..4)
+        const uint32_t lmask = ~(0xffffffffu << ((8u * nb) & 31u)) | (0u - (uint32_t)(nb == 4u));
+        const uint32_t n_lit = (mlong & ((b14 & lmask) + 1u)) | (~mlong & (x + 1u));
+        const uint32_t n_cp = (m1 & (4u + (x & 7u))) | (~m1 & (x + 1u));
+        const uint32_t n = (mlit & n_lit) | (~mlit & n_cp);
+        const uint32_t adv = (mlit & (1u + nb)) | (~mlit & (ty + 1u + (uint32_t)(ty == 3u)));
+        const uint32_t off = (m1 & (((tag & 0xe0u) << 3) | (b14 & 0xffu))) | (m2 & (b14 & 0xffffu)) | (~(m1 | m2) & b14);
         const uint32_t rem = se - s;  // >= 1
-        const bool bad = adv > rem || l64 > (uint64_t)(dlen - d) ||
-                         (lit ? l64 > (uint64_t)(rem - adv) : (off == 0u || off > d));
-        if (bad) {
-            ok = false;
+        // checks of decode_other.go (n == 0 only for a 4-byte literal length of 2^32 - 1: too long)
+        const uint32_t bad_lit = (uint32_t)(n > rem - adv), bad_cp = (uint32_t)(off == 0u) | (uint32_t)(off > d);
+        const bool bad = ((uint32_t)(adv > rem) | (uint32_t)(n > dlen - d) | (uint32_t)(n == 0u) |
+                          (mlit & bad_lit) | (~mlit & bad_cp)) != 0u;
+        const uint32_t sn = s + adv + (mlit & n);
+        const bool spill = op + d + n + 64u > sn;  // writes reach [op + d, op + d + n + 64); the next tag is at sn
+        if (bad | spill) {
+            res = bad ? 1u : 2u;
             break;
         }
-        const uint32_t n = (uint32_t)l64;
-        const uint32_t sn = s + adv + (lit ? n : 0u);
-        const uint64_t t8n = sn < se ? *reinterpret_cast<const u64_lds_u *>(lds + sn) : 0;  // next tag, in flight
-        const uint32_t a = lit ? s + adv : op + d - off;
+        const uint64_t t8n = *reinterpret_cast<const u64_lds_u *>(lds + sn);  // next tag, in flight
+        const uint32_t a = (mlit & (s + adv)) | (~mlit & (op + d - off));
         const uint32_t o = op + d;
-        const uint32_t sstep = lit ? 64u : 0u;
-        const uint32_t dstep = lit ? 64u : (off < n ? off : n);
+        const uint32_t sstep = mlit & 64u;
+        const uint32_t dstep = (mlit & 64u) | (~mlit & (off < n ? off : n));
         for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep) {
             const u32x4 c0 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
             const u32x4 c1 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 16);
@@ -332,29 +355,27 @@ __device__ __forceinline__ bool snappy_walk_lds(uint8_t *lds, uint32_t sp, uint3
         s = sn;
         t8 = t8n;
     }
-    return ok && d == dlen;
+    return res ? res : (d == dlen ? 0u : 1u);
 }
 
 }  // namespace
 
-template <int BPW, int SO, int OB>
+template <int BPW, int SLOT>
 __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off) {
-    static_assert(SO % 16 == 0 && OB % 16 == 0 && SO <= 1024 && OB <= 1024, "one 16-B chunk per lane per block");
-    constexpr uint32_t OUT = SO + 64, SLOT = SO + OB + 128;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT];
+    static_assert(SLOT % 16 == 0, "16-B aligned slots");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint64_t oend = (uint64_t)out_vals + out_cap;
     const uint32_t ngroups = (n + BPW - 1) / BPW;
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
     auto info = [&](uint32_t grp) -> SlInfo {
         const uint32_t i = grp * BPW + lane;
-        SlInfo r = sl_info<SO, OB>(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, base, out_cap);
+        SlInfo r = sl_info<SLOT>(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, base, out_cap);
         return r;
     };
     u32x4 v[BPW];
@@ -394,37 +415,29 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
                 x >>= 8 * sh;
                 c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
             }
-            if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + 16 * lane) = c;
+            if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 16 * lane) = c;
         }
         sl_wsync();
         // 2. descriptors of the group after next, then the next group's streams in flight
         const SlInfo nn = info(g + 2 * G);
         prefetch(nxt);
         // 3. decode
-        uint32_t fin = cur.status;
-        if (cur.mode == SL_LDS) {
-            uint8_t *const slot = lds + lane * SLOT;
+        uint32_t fin = cur.status, mode = cur.mode;
+        if (mode == SL_LDS) {
+            const uint32_t sb = lane * SLOT, sp = sb + sl_pos<SLOT>(cur.clen);
             uint32_t hdr = 0;
-            while (hdr < 5 && slot[hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
+            while (hdr < 5 && lds[sp + hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
             hdr++;
-            const uint32_t sb = lane * SLOT;
-            if (!snappy_walk_lds(lds, sb + hdr, sb + cur.clen, sb + OUT, cur.dlen)) fin = BHG_ST_SNAPPY_CORRUPT;
-        } else if (cur.mode == SL_GLOBAL) {
-            uint32_t hdr = 0;
-            for (;;) {
-                const uint32_t bb = gld<uint8_t>(cur.cp + hdr);
-                hdr++;
-                if (bb < 0x80) break;
-            }
-            if (!snappy_decode_rt(cur.cp + hdr, cur.clen - hdr, (uint64_t)out_vals + cur.o0, cur.dlen, end, oend))
-                fin = BHG_ST_SNAPPY_CORRUPT;
-        } else if (cur.mode == SL_TOOLARGE) {
+            const uint32_t r = snappy_walk_lds(lds, sp + hdr, sp + cur.clen, sb, cur.dlen);
+            if (r == 1) fin = BHG_ST_SNAPPY_CORRUPT;
+            if (r == 2) mode = SL_GLOBAL;
+        } else if (mode == SL_TOOLARGE) {
             fin = BHG_ST_SNAPPY_TOO_LARGE;
         }
         // 4. decoded blocks -> out_vals
         sl_wsync();
         {
-            const bool good = cur.mode == SL_LDS && (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH);
+            const bool good = mode == SL_LDS && (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH);
             const uint32_t dl = good ? cur.dlen : 0u;
 #pragma unroll
             for (int b = 0; b < BPW; b++) {
@@ -433,14 +446,14 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
                     const uint64_t ob = (uint64_t)out_vals +
                                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)cur.o0, b) |
                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(cur.o0 >> 32), b) << 32));
-                    st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + OUT + 16 * lane),
+                    st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + 16 * lane),
                               ob + dlb);
                 }
             }
         }
         sl_wsync();
-        // 5. descriptors
-        if (cur.mode != SL_SKIP) {
+        // 5. descriptors (SL_GLOBAL blocks stay provisional for the k_snappy_rt pass)
+        if (mode == SL_LDS || mode == SL_TOOLARGE) {
             uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
             dw[2] = 0;
             dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? cur.dlen : 0u;
@@ -454,16 +467,17 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
     if (BHG_SNAPPY_LDS && src_len >= 64) {
-        constexpr uint32_t BPW = BHG_SL_BPW, SO = BHG_SL_SO, OB = 1024;
-        constexpr uint32_t lds_bytes = BPW * (SO + OB + 128);
+        constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
+        constexpr uint32_t lds_bytes = BPW * SLOT + 64;
         const uint32_t per_cu = (160u * 1024u) / lds_bytes;
         const uint32_t groups = (n + BPW - 1) / BPW;
         const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
         uint32_t grid = groups < cap ? groups : cap;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_snappy_lds<BPW, SO, OB>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+        hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
                            out_vals, out_cap, val_off);
-        return hipGetLastError();
+        if (hipError_t e = hipGetLastError()) return e;
+        // then the blocks too big for a slot, lane per block from global memory
     }
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * 8;

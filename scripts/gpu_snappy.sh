@@ -14,3 +14,5 @@ for v in ${VARIANTS:-}; do
   BHG_LIB_PATH=$PWD/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 240 python -u bench.py --config c3 --no-cpu --no-e2e > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 1; }
   echo "$v: $(cut -c1-300 $O/c3_$v.json)"
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-e2e --steps 20 --warmup 20 > $O/c3_prof.json 2> $O/c3_prof.err || { tail -5 $O/c3_prof.err; exit 1; }
+f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp $f $O/c3_kernel_stats.csv; cut -d, -f1-8 $O/c3_kernel_stats.csv | head -8
