@@ -24,6 +24,24 @@ inline uint32_t lane_grid(const Launch &L, uint64_t n, uint32_t block) {
     return g == 0 ? 1u : (uint32_t)g;
 }
 
+// Workgroups of `block` threads of `kernel` that are resident on one CU at once: the
+// runtime's occupancy figure, capped by 160 KiB of LDS in 1-KiB allocation granules
+// (MI355X; the runtime figure alone over-counted k_snappy_enc: 12 where 11 fit, and the
+// 12th wave of each CU then ran after the others, +38 % time).  `fallback` if the queries fail.
+inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback) {
+    int b = 0;
+    hipFuncAttributes fa;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block, 0) != hipSuccess || b <= 0 ||
+        hipFuncGetAttributes(&fa, kernel) != hipSuccess)
+        return fallback;
+    const size_t lds = (fa.sharedSizeBytes + 1023) & ~(size_t)1023;
+    if (lds) {
+        const int by_lds = (int)((160u * 1024u) / lds);
+        if (by_lds < b) b = by_lds;
+    }
+    return b > 0 ? (uint32_t)b : 1u;
+}
+
 // bhg_decode.hip: descriptors for codec NONE (complete) or the snappy header
 // pass (sizes[i] = decoded length; the values follow with launch_snappy)
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

@@ -468,8 +468,10 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
     if (BHG_SNAPPY_LDS && src_len >= 64) {
         constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
-        constexpr uint32_t lds_bytes = BPW * SLOT + 64;
-        const uint32_t per_cu = (160u * 1024u) / lds_bytes;
+        // resident workgroups per CU (LDS-bound: 8 at 17 x 1,152 B); a grid past that would
+        // start its extra workgroups only when the first ones finish
+        static const uint32_t per_cu =
+            resident_per_cu((const void *)k_snappy_lds<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
         const uint32_t groups = (n + BPW - 1) / BPW;
         const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
         uint32_t grid = groups < cap ? groups : cap;

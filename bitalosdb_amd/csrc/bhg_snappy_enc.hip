@@ -20,7 +20,7 @@ namespace bhg {
 
 typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_U16
-#define BHG_SE_U16 0
+#define BHG_SE_U16 1  // measured with the register skip offsets: 49.4 GiB/s (11 waves/CU) vs 37.7 (u32, 7)
 #endif
 #ifndef BHG_SE_STAGE16
 #define BHG_SE_STAGE16 1  // measured: C4 30.7 vs 30.0 GiB/s (u16 table: 28.1 at 7 waves, 26.5 at 12)
@@ -56,9 +56,13 @@ __constant__ SkipTab kSkip = SkipTab();
 
 __device__ __forceinline__ uint32_t se_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
 
+// one (unaligned) ds_read_b32: gfx950 LDS takes unaligned dword reads
+typedef uint32_t u32_lds_u __attribute__((aligned(1), may_alias));
 __device__ __forceinline__ uint32_t lds_ld32(const uint8_t *b, uint32_t i) {
-    return (uint32_t)b[i] | ((uint32_t)b[i + 1] << 8) | ((uint32_t)b[i + 2] << 16) | ((uint32_t)b[i + 3] << 24);
+    return *reinterpret_cast<const u32_lds_u *>(b + i);
 }
+// lane i's value for a wave-uniform i: v_readlane, not an LDS permute
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
 
 struct Out {
     uint8_t *g;   // global destination of this value's stream
@@ -115,7 +119,13 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
 // encodeBlock on an LDS-staged block (len in [17, SE_CAP]); tab zeroed by the caller.
-__device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane) {
+// this lane's skip offsets F[64 j + lane] and F[64 j + lane + 1], j < 16 (k < 1024)
+struct LaneSkip {
+    uint32_t f[16], f1[16];
+};
+
+__device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
+                             const LaneSkip &F) {
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
     const uint32_t tmask = 16383;
@@ -126,29 +136,36 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         uint32_t cand = 0;
         bool remainder = false;
         for (uint32_t kb = 0;; kb += 64) {
-            const uint32_t k = kb + lane;
-            const uint32_t fk = k < 1024 ? kSkip.f[k] : 0x7fffffffu;
-            const uint32_t fk1 = k < 1024 ? kSkip.f[k + 1] : 0x7fffffffu;
+            // skip offsets from registers: a global load here would make the wave wait
+            // (vmcnt counts stores on gfx950) for every byte of output emitted so far
+            uint32_t fk = 0x7fffffffu, fk1 = 0x7fffffffu;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++)
+                if (kb == 64 * j) {
+                    fk = F.f[j];
+                    fk1 = F.f1[j];
+                }
             const uint64_t pos64 = (uint64_t)s + fk, nxt64 = (uint64_t)s + fk1;
             const bool valid = nxt64 <= sLimit;
             const uint32_t pos = valid ? (uint32_t)pos64 : 0u;
             const uint32_t u = lds_ld32(in, pos);
             const uint32_t h = se_hash(u, shift) & tmask;
-            // bucket duplicates inside the batch (latest earlier lane wins)
-            const uint32_t slot = h & 255;
-            if (valid) atomicAdd(&dcnt[slot], 1u);
+            // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
+            // of h mod 1024, one byte per bucket (<= 64 adds per byte)
+            const uint32_t slot = (h >> 2) & 255u, sh8 = 8 * (h & 3);
+            if (valid) atomicAdd(&dcnt[slot], 1u << sh8);
             wsync();
-            const bool maybe_dup = valid && dcnt[slot] > 1;
+            const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
             const uint64_t dm0 = __ballot(maybe_dup);
             uint64_t dm = dm0;
             uint32_t c = valid ? tab[h] : 0u;
             while (dm) {
                 const uint32_t i = __builtin_ctzll(dm);
                 dm &= dm - 1;
-                const uint32_t hi = __shfl(h, i, 64), pi = __shfl(pos, i, 64);
+                const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
                 if (valid && lane > i && hi == h) c = pi;   // lanes visited in increasing i: last wins
             }
-            if (valid) atomicSub(&dcnt[slot], 1u);
+            if (valid) atomicSub(&dcnt[slot], 1u << sh8);
             wsync();
             const bool m = valid && lds_ld32(in, c) == u;
             const uint64_t ev = __ballot(!valid || m);
@@ -162,7 +179,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             while (dm) {
                 const uint32_t i = __builtin_ctzll(dm);
                 dm &= dm - 1;
-                if (__shfl(h, i, 64) == h && i > lane) last = false;
+                if (lane_val(h, i) == h && i > lane) last = false;
             }
             if (last) tab[h] = (se_tab_t)pos;
 #else
@@ -170,57 +187,80 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
 #endif
             wsync();
             if (js < 64) {
-                const bool is_match = __shfl((int)m, js, 64) != 0;
+                const bool is_match = lane_val((uint32_t)m, js) != 0;
                 if (!is_match) { remainder = true; break; }
-                s = uni(__shfl(pos, js, 64));
-                cand = uni(__shfl(c, js, 64));
+                s = lane_val(pos, js);
+                cand = lane_val(c, js);
                 break;
             }
         }
         if (remainder) break;
         se_emit_literal(o, in + nextEmit, nullptr, s - nextEmit, lane);
         // ---- copies: emit, then check for an immediate next match ----
+        // encode_other.go's inner loop with two LDS round trips per copy: the table
+        // read for currHash (its hash input comes from the lanes' registers), then one
+        // compare of in[cand + t] with in[s + t] for t < 64 that both verifies the
+        // 4-byte match and extends it (Go's extension starts at s + 4 after a verified
+        // 4-byte match: the same first mismatch).
         bool to_rem = false;
+        uint32_t f;  // first mismatch of in[cand + t] vs in[s + t] (t < 64 per round)
+        uint32_t bt; // this lane's in[s + lane] of the round that found f
+        {
+            const uint32_t t = lane;
+            const uint32_t a = s + t < len ? in[cand + t] : 0u, b = in[s + t];
+            bt = b;
+            const uint64_t mm = __ballot(s + t >= len || a != b);
+            f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
+        }
         for (;;) {
             const uint32_t base = s;
-            s += 4;
-            // extend: first t with s+t == len or in[cand+4+t] != in[s+t]
-            uint32_t i0 = cand + 4;
-            for (;;) {
+            uint32_t fb = f;  // mismatch relative to the round's start
+            uint32_t r0 = s;  // start of the round that found fb
+            while (fb == 64u) {  // all 64 equal: next round
+                r0 += 64;
                 const uint32_t t = lane;
-                const bool inr = s + t < len;
-                bool neq = true;
-                if (inr) neq = in[i0 + t] != in[s + t];
-                const uint64_t mm = __ballot(neq);
-                if (mm) { const uint32_t f = (uint32_t)__builtin_ctzll(mm); s += f; break; }
-                s += 64;
-                i0 += 64;
+                const uint32_t a = r0 + t < len ? in[cand + (r0 - base) + t] : 0u, b = in[r0 + t];
+                bt = b;
+                const uint64_t mm = __ballot(r0 + t >= len || a != b);
+                fb = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
             }
+            s = r0 + fb;
             se_emit_copy(o, base - cand, s - base, lane);
             nextEmit = s;
             if (s >= sLimit) { to_rem = true; break; }
-            const uint32_t x0 = lds_ld32(in, s - 1), x4 = lds_ld32(in, s + 3);
-            const uint64_t x = (uint64_t)x0 | ((uint64_t)x4 << 32);
+            // x = in[s - 1 .. s + 7]: from the lanes of the last round when they hold it
+            uint64_t x;
+            const uint32_t k = s - 1 - r0;  // lane holding in[s - 1]
+            if (s - 1 >= r0 && k + 8 < 64u) {
+                x = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) x |= (uint64_t)(__builtin_amdgcn_readlane(bt, k + j) & 0xffu) << (8 * j);
+            } else {
+                x = (uint64_t)lds_ld32(in, s - 1) | ((uint64_t)lds_ld32(in, s + 3) << 32);
+            }
             const uint32_t prevHash = se_hash((uint32_t)x, shift) & tmask;
-#if BHG_SE_U16
-            if (lane == 0) tab[prevHash] = (se_tab_t)(s - 1);
-#else
-            if (lane == 0) atomicMax(&tab[prevHash], s - 1);
-#endif
-            wsync();
             const uint32_t currHash = se_hash((uint32_t)(x >> 8), shift) & tmask;
-            cand = uni(tab[currHash]);
+            const uint32_t tc = tab[currHash];  // read before the two stores (program order); prevHash == currHash gives s - 1
             wsync();
-#if BHG_SE_U16
-            if (lane == 0) tab[currHash] = (se_tab_t)s;
-#else
-            if (lane == 0) atomicMax(&tab[currHash], s);
-#endif
+            if (lane == 0) {
+                tab[prevHash] = (se_tab_t)(s - 1);
+                tab[currHash] = (se_tab_t)s;
+            }
+            const uint32_t c = uni(prevHash == currHash ? s - 1 : tc);
             wsync();
-            if ((uint32_t)(x >> 8) != lds_ld32(in, cand)) {
+            // verify in[c .. c + 4) == in[s .. s + 4) and extend in the same compare
+            {
+                const uint32_t t = lane;
+                const uint32_t a = s + t < len ? in[c + t] : 0u, b = in[s + t];
+                bt = b;
+                const uint64_t mm = __ballot(s + t >= len || a != b);
+                f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
+            }
+            if (f < 4u) {
                 s += 1;
                 break;
             }
+            cand = c;
         }
         if (to_rem) break;
     }
@@ -285,6 +325,12 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
     __shared__ uint32_t dcnt[256];
     const uint32_t lane = threadIdx.x;
     for (uint32_t j = lane; j < 256; j += 64) dcnt[j] = 0;
+    LaneSkip F;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) {
+        F.f[j] = kSkip.f[64 * j + lane];
+        F.f1[j] = kSkip.f[64 * j + lane + 1];
+    }
     uint16_t *gt = gtables + (size_t)blockIdx.x * 16384;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
@@ -336,7 +382,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                 while (ts < 16384 && ts < blen) ts *= 2;
                 for (uint32_t t = lane; t < ts; t += 64) tab[t] = 0;
                 wsync();
-                se_block_lds(o, in, blen, tab, dcnt, lane);
+                se_block_lds(o, in, blen, tab, dcnt, lane, F);
             } else {
                 uint32_t d = o.d;
                 if (lane == 0) {
@@ -363,8 +409,12 @@ hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32
     return hipGetLastError();
 }
 
+// one wave per resident workgroup slot (LDS: 13 KiB per wave with the u16 table, 21 KiB
+// with u32 -- 11 / 7 per CU on MI355X): a grid past what is resident would start its extra
+// workgroups only when the first ones finish
 uint32_t snappy_enc_grid(const Launch &L, uint32_t n) {
-    uint32_t g = (uint32_t)L.num_cus * BHG_SE_WAVES;  // LDS: 21 KiB per wave (u32 table), 13 KiB (u16)
+    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc, 64, BHG_SE_WAVES);
+    uint32_t g = (uint32_t)L.num_cus * (uint32_t)per_cu;
     if (g > n) g = n;
     return g ? g : 1;
 }
