@@ -218,18 +218,20 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 //   3. lane b walks block b entirely in LDS;
 //   4. the wave stores each decoded block with contiguous 16-B stores;
 //   5. the descriptors are finalised.
-// The element step moves every element as "ops" of 64 B: 4 x 16-B reads from
-// the source, 4 x 16-B writes to the destination, no masking.
-//   literal:         op j reads stream + s + 64 j, writes out + d + 64 j
-//   copy, offset o:  op t reads out + d - o (the same 64 B every time),
-//                    writes out + d + t * min(o, n)
+// The element step moves every element as "ops" of 16 B (84 % of C3 elements
+// are <= 16 B), one 16-B read and one 16-B write, no masking:
+//   literal, or copy of offset o >= 16:  op j reads src + 16 j, writes d + 16 j
+//     (a copy's source of op j lies below d + 16 j: written by ops < j)
+//   copy of offset o < 16:  op t reads the 16 B at d - o (its first o bytes
+//     valid), writes them at d + t o
 // A write past the element's end lands in bytes later elements (or the pad)
-// own and is overwritten by them in program order; for an overlapping copy
-// (o < n) the last write to every byte of the element comes from the op whose
-// period contains it and reads only bytes below d or already final (LDS is in
-// order per wave, so a read sees every earlier write of its lane).  So every
-// byte of [0, dlen) ends up right, and a typical element is one op: one LDS
-// round trip, with the next tag's read in flight alongside it.
+// own and is overwritten by them in program order; for a short-offset copy
+// the last write to every byte comes from the op whose period holds it (LDS
+// is in order per wave, so a read sees every earlier write of its lane).  So
+// every byte of [0, dlen) ends up right, and a typical element is one op with
+// the next tag's read in flight alongside it.  (64-B ops measured 18 % slower:
+// 4x the LDS bytes, and unaligned LDS accesses stall -- PMC: 55 % of LDS-active
+// cycles; dword-aligned stores with a read-back head merge measured 21 % slower.)
 // Checks are the reference decoder's, as in snappy_decode_rt.
 // ---------------------------------------------------------------------------
 #ifndef BHG_SNAPPY_LDS
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // type-based alias analysis must not reorder those accesses.
 typedef uint64_t u64_lds_u __attribute__((aligned(1), may_alias));
 typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));
+
 
 namespace {
 
@@ -310,7 +313,10 @@ __device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc
 __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op,
                                                     uint32_t dlen) {
     uint32_t s = sp, d = 0, res = 0;
-    uint64_t t8 = *reinterpret_cast<const u64_lds_u *>(lds + s);
+    // the tag and the 4 bytes after it (one unaligned ds_read_b64; two aligned dword reads
+    // measured no faster)
+    auto tag_at = [&](uint32_t p) -> uint64_t { return *reinterpret_cast<const u64_lds_u *>(lds + p); };
+    uint64_t t8 = tag_at(s);
     while (s < se) {
         const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
         const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
@@ -336,21 +342,17 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
             res = bad ? 1u : 2u;
             break;
         }
-        const uint64_t t8n = *reinterpret_cast<const u64_lds_u *>(lds + sn);  // next tag, in flight
+        const uint64_t t8n = tag_at(sn);  // next tag, in flight
         const uint32_t a = (mlit & (s + adv)) | (~mlit & (op + d - off));
         const uint32_t o = op + d;
-        const uint32_t sstep = mlit & 64u;
-        const uint32_t dstep = (mlit & 64u) | (~mlit & (off < n ? off : n));
-        for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep) {
-            const u32x4 c0 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
-            const u32x4 c1 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 16);
-            const u32x4 c2 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 32);
-            const u32x4 c3 = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r + 48);
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = c0;
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 16) = c1;
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 32) = c2;
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t + 48) = c3;
-        }
+        // 16-B ops (84 % of C3 elements are <= 16 B): a literal or a copy of offset >= 16 moves
+        // 16 B at a time (a copy's op j reads bytes below o + 16 j, written by ops < j); a copy of
+        // offset < 16 writes the 16 B at a (its first `off` bytes valid) at o, o + off, ...
+        const uint32_t big = mlit | (0u - (uint32_t)(off >= 16u));
+        const uint32_t sstep = big & 16u;
+        const uint32_t dstep = (big & 16u) | (~big & off);
+        for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep)
+            *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
         d += n;
         s = sn;
         t8 = t8n;
