@@ -281,10 +281,12 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
     if (codec == BHG_CODEC_SNAPPY) {
         Scratch sc;
-        if (int r = scratch_alloc(c, L.stream, bhg::scan_scratch_bytes(n), sc)) return r;
+        const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
+        if (int r = scratch_alloc(c, L.stream, scan_b + (out_vals ? bhg::snappy_list_bytes(n) : 0), sc)) return r;
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
         if (out_vals)
-            HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off));
+            HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off,
+                                          reinterpret_cast<uint32_t *>(sc.base + scan_b)));
     }
     return BHG_OK;
 }
@@ -446,15 +448,17 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     const size_t hb = (size_t)n * sizeof(bhg_handle), db = (size_t)n * sizeof(bhg_desc);
     const size_t eb = expected_crc ? (size_t)n * 4 : 0, ob = codec == BHG_CODEC_SNAPPY ? ((size_t)n + 1) * 8 : 0;
     const size_t sb = codec == BHG_CODEC_SNAPPY ? bhg::scan_scratch_bytes(n) : 0;
+    const size_t lb = codec == BHG_CODEC_SNAPPY && out_vals ? bhg::snappy_list_bytes(n) : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     if (int r = ensure_buf(c, &c->h_src, &c->h_src_cap, src_len + 64)) return r;
-    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(sb) + 256)) return r;
+    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(sb) + al(lb) + 256)) return r;
     uint8_t *a = reinterpret_cast<uint8_t *>(c->h_aux);
     bhg_handle *dh = reinterpret_cast<bhg_handle *>(a); a += al(hb);
     bhg_desc *dd = reinterpret_cast<bhg_desc *>(a); a += al(db);
     uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(eb);
     uint64_t *doff = ob ? reinterpret_cast<uint64_t *>(a) : nullptr; a += al(ob);
-    void *dscan = sb ? a : nullptr;
+    void *dscan = sb ? a : nullptr; a += al(sb);
+    uint32_t *dlist = lb ? reinterpret_cast<uint32_t *>(a) : nullptr;
     hipStream_t s = c->stream;
     HIP_TRY(c, hipMemcpyAsync(c->h_src, src, src_len, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(dh, handles, hb, hipMemcpyHostToDevice, s));
@@ -472,7 +476,7 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
             if (total > out_vals_cap) total = out_vals_cap;
             if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 64)) return r;
             uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals);
-            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff));
+            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dlist));
             if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
         }
     }

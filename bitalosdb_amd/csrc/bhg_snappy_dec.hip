@@ -161,18 +161,21 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
 
 }  // namespace
 
+// list: null (every block) or {count, block indices...} (the blocks k_snappy_lds left)
 __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
-                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off) {
+                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off,
+                                                   const uint32_t *__restrict__ list) {
     const uint64_t base = (uint64_t)src, end = base + src_len;
     const uint64_t oend = (uint64_t)out_vals + out_cap;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t cnt = list ? list[0] : n;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
+        const uint32_t i = list ? list[1 + j] : j;
         uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
         const uint32_t status = dw[9];
         if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
         const uint32_t cpos = dw[2], dlen = dw[3];  // provisional: value position in the record, decoded length
-        if (cpos == 0) continue;  // finalised by k_snappy_lds (a provisional value position is >= 12)
         const bhg_handle h = handles[i];
         const uint64_t rec = base + h.offset;
         const uint32_t clen = h.length - cpos;
@@ -366,7 +369,8 @@ template <int BPW, int SLOT>
 __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
-                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off) {
+                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off,
+                                                   uint32_t *__restrict__ list) {
     static_assert(SLOT % 16 == 0, "16-B aligned slots");
     __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
@@ -454,7 +458,11 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             }
         }
         sl_wsync();
-        // 5. descriptors (SL_GLOBAL blocks stay provisional for the k_snappy_rt pass)
+        // 5. descriptors (SL_GLOBAL blocks stay provisional, listed for the k_snappy_rt pass)
+        if (mode == SL_GLOBAL) {
+            const uint32_t k = atomicAdd(list, 1u);
+            list[1 + k] = g * BPW + lane;
+        }
         if (mode == SL_LDS || mode == SL_TOOLARGE) {
             uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
             dw[2] = 0;
@@ -467,8 +475,10 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
 }
 
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                         bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off) {
-    if (BHG_SNAPPY_LDS && src_len >= 64) {
+                         bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
+                         uint32_t *list) {
+    if (BHG_SNAPPY_LDS && src_len >= 64 && list) {
+        if (hipError_t e = hipMemsetAsync(list, 0, 4, L.stream)) return e;
         constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
         // resident workgroups per CU (LDS-bound: 8 at 17 x 1,152 B); a grid past that would
         // start its extra workgroups only when the first ones finish
@@ -479,16 +489,19 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         uint32_t grid = groups < cap ? groups : cap;
         if (grid == 0) grid = 1;
         hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                           out_vals, out_cap, val_off);
+                           out_vals, out_cap, val_off, list);
         if (hipError_t e = hipGetLastError()) return e;
-        // then the blocks too big for a slot, lane per block from global memory
+        // then the blocks it listed (too big for a slot), lane per block from global memory
+        hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
+                           out_cap, val_off, (const uint32_t *)list);
+        return hipGetLastError();
     }
     uint32_t grid = (n + 255) / 256;
     const uint32_t cap = (uint32_t)L.num_cus * 8;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(k_snappy_rt, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals, out_cap,
-                       val_off);
+                       val_off, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 

@@ -190,6 +190,58 @@ def test_snappy_corrupt_streams(codec):
     assert list(exp["status"][6:]) == [0, 0]
 
 
+def _uvarint(x):
+    out = bytearray()
+    while x >= 0x80:
+        out.append(x & 0x7f | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+def test_snappy_inplace_spill_and_oversize(codec):
+    """The LDS decoder decodes in place (stream at the slot end, output from the
+    start).  A valid stream whose output runs far ahead of its stream -- 700 B of
+    RLE copies first, then 324 one-byte copies (3 stream bytes each) -- would
+    overwrite its own unread tags: the walk must hand it to the global-memory
+    pass.  Mixed with ordinary blocks, oversize blocks (> 1 KiB out) and
+    incompressible ones, so the fallback list holds a few blocks among many."""
+    rng = random.Random(21)
+    body = bytes([0 << 2]) + b"x"                      # literal "x"
+    body += (bytes([(64 - 1) << 2 | 2]) + (1).to_bytes(2, "little")) * 10   # 10 x copy-2, n 64, offset 1
+    body += bytes([(59 - 1) << 2 | 2]) + (1).to_bytes(2, "little")          # copy n 59 -> 700 B so far
+    body += (bytes([0 << 2 | 2]) + (7).to_bytes(2, "little")) * 324        # 324 x copy-2, n 1, offset 7
+    spill = _uvarint(1024) + body
+    assert len(spill) <= 1024
+    want = O.snappy_decode(spill)
+    assert want is not None and len(want) == 1024
+    streams = []
+    for i in range(3000):
+        k = i % 6
+        if k == 0:
+            streams.append(spill)
+        elif k == 1:
+            streams.append(O.snappy_encode(rand_bytes(rng, 1024)))         # incompressible: clen > 1 KiB
+        elif k == 2:
+            streams.append(O.snappy_encode(compressible(rng, 3000)))       # oversize output
+        else:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([16, 500, 1024]))))
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"spill%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert (exp["status"] == 0).all()
+    assert np.array_equal(goff, eoff)
+    assert gvals.tobytes() == evals[:int(eoff[-1])].tobytes()
+    assert gvals[int(goff[0]):int(goff[1])].tobytes() == want
+
+
 def test_known_answer_tables(codec):
     """K1 + K2 tables written by the restated writer, scanned, decoded on GPU."""
     rng = random.Random(9)
