@@ -340,7 +340,7 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
         const bool bad = ((uint32_t)(adv > rem) | (uint32_t)(n > dlen - d) | (uint32_t)(n == 0u) |
                           (mlit & bad_lit) | (~mlit & bad_cp)) != 0u;
         const uint32_t sn = s + adv + (mlit & n);
-        const bool spill = op + d + n + 64u > sn;  // writes reach [op + d, op + d + n + 64); the next tag is at sn
+        const bool spill = op + d + n + 16u > sn;  // 16-B ops write below op + d + n + 16; the next tag is at sn
         if (bad | spill) {
             res = bad ? 1u : 2u;
             break;
