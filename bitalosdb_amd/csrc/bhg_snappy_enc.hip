@@ -58,6 +58,7 @@ __device__ __forceinline__ uint32_t se_hash(uint32_t u, uint32_t shift) { return
 
 // one (unaligned) ds_read_b32: gfx950 LDS takes unaligned dword reads
 typedef uint32_t u32_lds_u __attribute__((aligned(1), may_alias));
+// (4 byte reads measured 5 % slower, two aligned dwords + a funnel shift the same)
 __device__ __forceinline__ uint32_t lds_ld32(const uint8_t *b, uint32_t i) {
     return *reinterpret_cast<const u32_lds_u *>(b + i);
 }
