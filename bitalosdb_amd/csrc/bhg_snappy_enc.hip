@@ -125,8 +125,14 @@ struct LaneSkip {
     uint32_t f[16], f1[16];
 };
 
+#ifdef BHG_SE_PROF
+__device__ uint64_t se_prof[8];  // lab: cycles in scan / literal emit / copy loop, counts
+#define SE_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#else
+#define SE_T(x)
+#endif
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
-                             const LaneSkip &F) {
+                             const LaneSkip &F, uint64_t *acc) {
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
     const uint32_t tmask = 16383;
@@ -136,6 +142,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         // ---- scan phase: iterations k = 0,1,... at positions s + F[k] ----
         uint32_t cand = 0;
         bool remainder = false;
+        SE_T(t_scan0);
         for (uint32_t kb = 0;; kb += 64) {
             // skip offsets from registers: a global load here would make the wave wait
             // (vmcnt counts stores on gfx950) for every byte of output emitted so far
@@ -195,8 +202,17 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 break;
             }
         }
+#ifdef BHG_SE_PROF
+        SE_T(t_scan1);
+        acc[0] += t_scan1 - t_scan0;
+        acc[3] += 1;
+#endif
         if (remainder) break;
         se_emit_literal(o, in + nextEmit, nullptr, s - nextEmit, lane);
+#ifdef BHG_SE_PROF
+        SE_T(t_lit1);
+        acc[1] += t_lit1 - t_scan1;
+#endif
         // ---- copies: emit, then check for an immediate next match ----
         // encode_other.go's inner loop with two LDS round trips per copy: the table
         // read for currHash (its hash input comes from the lanes' registers), then one
@@ -263,6 +279,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             }
             cand = c;
         }
+#ifdef BHG_SE_PROF
+        SE_T(t_cp1);
+        acc[2] += t_cp1 - t_lit1;
+#endif
         if (to_rem) break;
     }
     if (nextEmit < len) se_emit_literal(o, in + nextEmit, nullptr, len - nextEmit, lane);
@@ -333,6 +353,10 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
         F.f1[j] = kSkip.f[64 * j + lane + 1];
     }
     uint16_t *gt = gtables + (size_t)blockIdx.x * 16384;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef BHG_SE_PROF
+    const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
         if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
@@ -383,7 +407,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                 while (ts < 16384 && ts < blen) ts *= 2;
                 for (uint32_t t = lane; t < ts; t += 64) tab[t] = 0;
                 wsync();
-                se_block_lds(o, in, blen, tab, dcnt, lane, F);
+                se_block_lds(o, in, blen, tab, dcnt, lane, F, acc);
             } else {
                 uint32_t d = o.d;
                 if (lane == 0) {
@@ -395,7 +419,17 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
             }
         }
         if (lane == 0) clen[i] = o.d;
+        acc[4] += 1;
     }
+#ifdef BHG_SE_PROF
+    acc[5] = __builtin_amdgcn_s_memtime() - t_k0;
+    if (lane == 0)
+        for (int q = 0; q < 6; q++) atomicAdd((unsigned long long *)&se_prof[q], (unsigned long long)acc[q]);
+    if (blockIdx.x == 0 && lane == 0)
+        printf("se_prof wave0: scan %llu lit %llu copy %llu phases %llu values %llu total %llu\n",
+               (unsigned long long)acc[0], (unsigned long long)acc[1], (unsigned long long)acc[2],
+               (unsigned long long)acc[3], (unsigned long long)acc[4], (unsigned long long)acc[5]);
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_snappy_maxlen(const uint64_t *val_off, uint32_t n, uint64_t *out) {
