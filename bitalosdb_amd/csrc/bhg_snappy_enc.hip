@@ -146,13 +146,17 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         for (uint32_t kb = 0;; kb += 64) {
             // skip offsets from registers: a global load here would make the wave wait
             // (vmcnt counts stores on gfx950) for every byte of output emitted so far
-            uint32_t fk = 0x7fffffffu, fk1 = 0x7fffffffu;
+            uint32_t fk = F.f[0], fk1 = F.f1[0];
+            if (kb != 0) {  // wave-uniform; the first batch is by far the most common
+                fk = 0x7fffffffu;
+                fk1 = 0x7fffffffu;
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++)
-                if (kb == 64 * j) {
-                    fk = F.f[j];
-                    fk1 = F.f1[j];
-                }
+                for (uint32_t j = 1; j < 16; j++)
+                    if (kb == 64 * j) {
+                        fk = F.f[j];
+                        fk1 = F.f1[j];
+                    }
+            }
             const uint64_t pos64 = (uint64_t)s + fk, nxt64 = (uint64_t)s + fk1;
             const bool valid = nxt64 <= sLimit;
             const uint32_t pos = valid ? (uint32_t)pos64 : 0u;
@@ -161,21 +165,22 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
             // of h mod 1024, one byte per bucket (<= 64 adds per byte)
             const uint32_t slot = (h >> 2) & 255u, sh8 = 8 * (h & 3);
-            if (valid) atomicAdd(&dcnt[slot], 1u << sh8);
+            atomicAdd(&dcnt[slot], valid ? 1u << sh8 : 0u);  // unconditional: no exec-mask branch
             wsync();
             const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
             const uint64_t dm0 = __ballot(maybe_dup);
             uint64_t dm = dm0;
-            uint32_t c = valid ? tab[h] : 0u;
+            uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
             while (dm) {
                 const uint32_t i = __builtin_ctzll(dm);
                 dm &= dm - 1;
                 const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
                 if (valid && lane > i && hi == h) c = pi;   // lanes visited in increasing i: last wins
             }
-            if (valid) atomicSub(&dcnt[slot], 1u << sh8);
+            atomicSub(&dcnt[slot], valid ? 1u << sh8 : 0u);
             wsync();
-            const bool m = valid && lds_ld32(in, c) == u;
+            const bool eq = lds_ld32(in, c) == u;
+            const bool m = valid && eq;
             const uint64_t ev = __ballot(!valid || m);
             const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
             // table updates: iterations before the event, plus the event itself when it is a match
