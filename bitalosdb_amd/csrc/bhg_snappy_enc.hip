@@ -157,9 +157,9 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                         fk1 = F.f1[j];
                     }
             }
-            const uint64_t pos64 = (uint64_t)s + fk, nxt64 = (uint64_t)s + fk1;
-            const bool valid = nxt64 <= sLimit;
-            const uint32_t pos = valid ? (uint32_t)pos64 : 0u;
+            // s < 64 Ki and F[k] <= 2^31 - 1: the sums fit in 32 bits
+            const bool valid = s + fk1 <= sLimit;
+            const uint32_t pos = valid ? s + fk : 0u;
             const uint32_t u = lds_ld32(in, pos);
             const uint32_t h = se_hash(u, shift) & tmask;
             // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
@@ -226,11 +226,11 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         // 4-byte match: the same first mismatch).
         bool to_rem = false;
         uint32_t f;  // first mismatch of in[cand + t] vs in[s + t] (t < 64 per round)
-        uint32_t bt; // this lane's in[s + lane] of the round that found f
+        uint32_t bt; // this lane's in[r0 + lane .. + 4) of the round that found f
         {
             const uint32_t t = lane;
-            const uint32_t a = s + t < len ? in[cand + t] : 0u, b = in[s + t];
-            bt = b;
+            const uint32_t bw = lds_ld32(in, s + t), a = in[cand + t], b = bw & 0xffu;  // past len: forced mismatch
+            bt = bw;
             const uint64_t mm = __ballot(s + t >= len || a != b);
             f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
         }
@@ -241,8 +241,8 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             while (fb == 64u) {  // all 64 equal: next round
                 r0 += 64;
                 const uint32_t t = lane;
-                const uint32_t a = r0 + t < len ? in[cand + (r0 - base) + t] : 0u, b = in[r0 + t];
-                bt = b;
+                const uint32_t bw = lds_ld32(in, r0 + t), a = in[cand + (r0 - base) + t], b = bw & 0xffu;
+                bt = bw;
                 const uint64_t mm = __ballot(r0 + t >= len || a != b);
                 fb = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
             }
@@ -250,13 +250,11 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             se_emit_copy(o, base - cand, s - base, lane);
             nextEmit = s;
             if (s >= sLimit) { to_rem = true; break; }
-            // x = in[s - 1 .. s + 7]: from the lanes of the last round when they hold it
+            // x = in[s - 1 .. s + 7): lane t of the last round holds in[r0 + t .. r0 + t + 4)
             uint64_t x;
             const uint32_t k = s - 1 - r0;  // lane holding in[s - 1]
-            if (s - 1 >= r0 && k + 8 < 64u) {
-                x = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 8; j++) x |= (uint64_t)(__builtin_amdgcn_readlane(bt, k + j) & 0xffu) << (8 * j);
+            if (s - 1 >= r0 && k + 4 < 64u) {
+                x = (uint64_t)lane_val(bt, k) | ((uint64_t)lane_val(bt, k + 4) << 32);
             } else {
                 x = (uint64_t)lds_ld32(in, s - 1) | ((uint64_t)lds_ld32(in, s + 3) << 32);
             }
@@ -273,8 +271,8 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // verify in[c .. c + 4) == in[s .. s + 4) and extend in the same compare
             {
                 const uint32_t t = lane;
-                const uint32_t a = s + t < len ? in[c + t] : 0u, b = in[s + t];
-                bt = b;
+                const uint32_t bw = lds_ld32(in, s + t), a = in[c + t], b = bw & 0xffu;
+                bt = bw;
                 const uint64_t mm = __ballot(s + t >= len || a != b);
                 f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
             }
