@@ -12,7 +12,10 @@
 // The branch-light walk (snappy_decode_lds2) is bit-exact in a host emulation
 // (scripts: 200k fuzzed streams + C3 values) but its BPW=20 build aborted twice
 // on the GPU inside tests/test_gpu_decode.py::test_snappy_values and passed once
-// in isolation -- cause not found; not measured further.  Kept here as the record.
+// in isolation.  Cause found in session 3 (the product k_snappy_lds hit it too):
+// `(uint64_t)__builtin_amdgcn_readlane(lo32, b)` sign-extends (readlane returns int)
+// an address whose bit 31 is set, and lanes that hand LDS bytes to each other need
+// a wavefront fence + may_alias LDS types.  Kept here as the record.
 #include "../../bitalosdb_amd/csrc/bhg_device.h"
 
 namespace bhg {
