@@ -1,0 +1,137 @@
+"""CPU check of the LDS snappy element walk (k_snappy_lds, bhg_snappy_dec.hip):
+the device function `snappy_walk_lds` is extracted from the product source,
+compiled for the host with clang, and run on an LDS-shaped byte array laid out
+as the kernel lays out an in-place slot (output from the slot start, stream
+staged at the slot end).  Every result must be the restated golang/snappy
+decode (oracle, parity pinned by pyarrow interop in test_oracle_snappy.py),
+SNAPPY_CORRUPT exactly where the restatement rejects, or a hand-over to the
+global-memory pass (2) -- never wrong bytes.  No GPU involved; the GPU run of
+the same code is tests/test_gpu_decode.py."""
+import ctypes
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "bitalosdb_amd", "csrc", "bhg_snappy_dec.hip")
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+SLOT = 1152  # BHG_SL_SLOT
+
+
+@pytest.fixture(scope="module")
+def walk(tmp_path_factory):
+    if not os.path.exists(CLANG):
+        pytest.skip("no clang++")
+    s = open(SRC).read()
+    i0 = s.index("__device__ __forceinline__ uint32_t snappy_walk_lds(")
+    i1 = s.index("}  // namespace\n\ntemplate <int BPW")
+    body = s[i0:i1].replace("__device__ __forceinline__ ", 'extern "C" ')
+    hdr = ("#include <stdint.h>\n"
+           "typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));\n"
+           "typedef uint64_t u64_lds_u __attribute__((aligned(1), may_alias));\n"
+           "typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));\n")
+    d = tmp_path_factory.mktemp("walk")
+    cpp, so = d / "walk.cpp", d / "walk.so"
+    cpp.write_text(hdr + body)
+    subprocess.check_call([CLANG, "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(so), str(cpp)])
+    lib = ctypes.CDLL(str(so))
+    lib.snappy_walk_lds.restype = ctypes.c_uint32
+    lib.snappy_walk_lds.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 4
+    return lib
+
+
+def run_slot(walk, stream, dlen):
+    """Stage `stream` as k_snappy_lds does and walk it; returns (code, output bytes)."""
+    clen = len(stream)
+    pos = (SLOT - 8 - ((clen + 15) & ~15)) & ~15
+    lds = np.zeros(2 * SLOT + 64, dtype=np.uint8)   # the slot, then a neighbour slot and the pad
+    lds[pos:pos + clen] = np.frombuffer(stream, dtype=np.uint8)
+    hdr = 0
+    while hdr < 5 and lds[pos + hdr] >= 0x80:
+        hdr += 1
+    hdr += 1
+    r = walk.snappy_walk_lds(lds.ctypes.data, pos + hdr, pos + clen, 0, dlen)
+    return r, lds[:dlen].tobytes()
+
+
+def uvarint(x):
+    out = bytearray()
+    while x >= 0x80:
+        out.append(x & 0x7f | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+def values(rng, k):
+    for i in range(k):
+        n = rng.choice([1, 4, 15, 16, 17, 63, 64, 65, 100, 500, 1000, 1024])
+        kind = i % 5
+        if kind == 0:
+            yield bytes(rng.getrandbits(8) for _ in range(n))              # literals only
+        elif kind == 1:
+            yield bytes(rng.choice(b"ab") for _ in range(n))              # short-offset copies
+        elif kind == 2:
+            yield (b"0123456789abcdefXYZ" * 60)[:n]                       # period 19
+        else:                                                             # 16-B words, the C3 shape
+            words = [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(8)]
+            yield b"".join(rng.choice(words) if rng.random() > 0.25 else
+                           bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(64))[:n]
+
+
+def test_walk_matches_restated_decode(walk):
+    rng = random.Random(5)
+    codes = {0: 0, 1: 0, 2: 0}
+    for v in values(rng, 1500):
+        st = O.snappy_encode(v)
+        if len(st) + 24 > SLOT or len(v) > 1024:
+            continue                       # not staged: the kernel sends it to k_snappy_rt
+        r, out = run_slot(walk, st, len(v))
+        codes[r] += 1
+        assert r != 1
+        if r == 0:
+            assert out == v
+    assert codes[0] > 1000
+
+
+def test_walk_hands_over_when_output_overtakes_stream(walk):
+    body = bytes([0]) + b"x"
+    body += (bytes([(64 - 1) << 2 | 2]) + (1).to_bytes(2, "little")) * 10
+    body += bytes([(59 - 1) << 2 | 2]) + (1).to_bytes(2, "little")
+    body += (bytes([2]) + (7).to_bytes(2, "little")) * 324      # 324 one-byte copies, 3 B of stream each
+    st = uvarint(1024) + body
+    assert O.snappy_decode(st) is not None
+    r, _ = run_slot(walk, st, 1024)
+    assert r == 2
+
+
+def test_walk_rejects_what_the_restatement_rejects(walk):
+    rng = random.Random(6)
+    good = O.snappy_encode(b"".join(bytes([rng.getrandbits(8)]) * 9 for _ in range(100)))
+    cases = [
+        good[:-1],                                       # truncated
+        uvarint(5) + bytes([0]) + b"a" + bytes([1, 0]),  # copy-1 with offset 0
+        uvarint(5) + bytes([0, 1]),                      # short output
+        uvarint(8) + bytes([60 << 2]),                   # truncated literal length
+        uvarint(4) + bytes([3 << 2]) + b"abc" + bytes([1 << 2 | 1, 9]),   # offset past the output
+        uvarint(2) + bytes([2 << 2]) + b"abc",           # literal past dlen
+    ]
+    walked = 0
+    for st in cases:
+        with pytest.raises(O.SnappyCorrupt):
+            O.snappy_decode(st)
+        try:
+            dl, _ = O.snappy_decoded_len(st)
+        except O.SnappyCorrupt:
+            continue                       # rejected by the header pass before any walk
+        if dl > 1024:
+            continue
+        r, _ = run_slot(walk, st, dl)
+        assert r in (1, 2), st
+        walked += 1
+    assert walked >= 4
