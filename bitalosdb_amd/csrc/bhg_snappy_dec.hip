@@ -323,17 +323,19 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
     while (s < se) {
         const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
         const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
-        // all-ones masks instead of ?: so the compiler keeps this straight-line
-        const uint32_t mlit = 0u - (uint32_t)(ty == 0u), m1 = 0u - (uint32_t)(ty == 1u),
-                       m2 = 0u - (uint32_t)(ty == 2u);
-        const uint32_t mlong = mlit & (0u - (uint32_t)(x >= 60u));
-        const uint32_t nb = (x - 59u) & mlong;  // length bytes of a long literal (1..4)
-        const uint32_t lmask = ~(0xffffffffu << ((8u * nb) & 31u)) | (0u - (uint32_t)(nb == 4u));
-        const uint32_t n_lit = (mlong & ((b14 & lmask) + 1u)) | (~mlong & (x + 1u));
-        const uint32_t n_cp = (m1 & (4u + (x & 7u))) | (~m1 & (x + 1u));
-        const uint32_t n = (mlit & n_lit) | (~mlit & n_cp);
-        const uint32_t adv = (mlit & (1u + nb)) | (~mlit & (ty + 1u + (uint32_t)(ty == 3u)));
-        const uint32_t off = (m1 & (((tag & 0xe0u) << 3) | (b14 & 0xffu))) | (m2 & (b14 & 0xffffu)) | (~(m1 | m2) & b14);
+        // per-type constants from shifts of packed nibble/byte tables (straight-line; the
+        // ?: form compiled to per-type exec-mask branches):
+        //   adv: literal 1, copy-1 2, copy-2 3, copy-4 5;  offset mask: ~0 >> {-, 24, 16, 0}
+        const uint32_t mlit = 0u - (uint32_t)(ty == 0u), m1 = 0u - (uint32_t)(ty == 1u);
+        uint32_t n = (m1 & (4u + (x & 7u))) | (~m1 & (x + 1u));
+        uint32_t adv = (0x5321u >> (4u * ty)) & 0xfu;
+        const uint32_t off = (b14 & (0xffffffffu >> ((0x00101800u >> (8u * ty)) & 0xffu))) | (m1 & ((tag >> 5) << 8));
+        if (ty == 0u && x >= 60u) {  // long literal: 1-4 length bytes (rare; divergent)
+            const uint32_t nb = x - 59u;
+            const uint32_t lmask = nb >= 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u);
+            n = (b14 & lmask) + 1u;
+            adv = 1u + nb;
+        }
         const uint32_t rem = se - s;  // >= 1
         // checks of decode_other.go (n == 0 only for a 4-byte literal length of 2^32 - 1: too long)
         const uint32_t bad_lit = (uint32_t)(n > rem - adv), bad_cp = (uint32_t)(off == 0u) | (uint32_t)(off > d);
