@@ -208,12 +208,13 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // A workgroup is one wave and owns BPW LDS slots of SLOT bytes.  The block
 // decodes IN PLACE: its output grows from the slot start, its stream is staged
 // at the slot end (P = (SLOT - 8 - round16(clen)) & ~15), and the walk checks
-// before every element that its writes (which overshoot by up to 63 B) stay
+// before every element that its writes (which overshoot by up to 15 B) stay
 // below the next unread tag; a block that would break that (or does not fit)
-// is left for the lane-per-block k_snappy_rt pass from global memory.  At C3
-// (1 KiB values, streams <= 721 B) a 1,152-B slot never falls back, so 140
-// blocks are resident per CU instead of 80 with separate stream and output
-// areas.  Per group of BPW consecutive blocks:
+// is listed for the lane-per-block k_snappy_rt pass from global memory.  At C3
+// (1 KiB values, streams <= 721 B) a 1,088-B slot never falls back, so 144
+// blocks are resident per CU (8 waves x 18) instead of 80 with separate
+// stream and output areas (measured: 1,152-B slots x 17 blocks 1.080 ms per C3
+// step, 1,088 x 18 1.044, 1,088 x 17 1.077, 1,072 x 19 1.178).  Per group of BPW consecutive blocks:
 //   1. the group's streams (prefetched into VGPRs, one 16-B chunk per lane per
 //      block) are written into the slots;
 //   2. the NEXT group's streams are requested (loads in flight during 3-5),
@@ -241,10 +242,10 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 #define BHG_SNAPPY_LDS 1
 #endif
 #ifndef BHG_SL_BPW
-#define BHG_SL_BPW 17
+#define BHG_SL_BPW 18
 #endif
 #ifndef BHG_SL_SLOT
-#define BHG_SL_SLOT 1152
+#define BHG_SL_SLOT 1088
 #endif
 
 // Every LDS access of k_snappy_lds goes through these may_alias types: the slot
@@ -482,7 +483,7 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
     if (BHG_SNAPPY_LDS && src_len >= 64 && list) {
         if (hipError_t e = hipMemsetAsync(list, 0, 4, L.stream)) return e;
         constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
-        // resident workgroups per CU (LDS-bound: 8 at 17 x 1,152 B); a grid past that would
+        // resident workgroups per CU (LDS-bound: 8 at 18 x 1,088 B); a grid past that would
         // start its extra workgroups only when the first ones finish
         static const uint32_t per_cu =
             resident_per_cu((const void *)k_snappy_lds<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
