@@ -25,16 +25,18 @@ inline uint32_t lane_grid(const Launch &L, uint64_t n, uint32_t block) {
 }
 
 // Workgroups of `block` threads of `kernel` that are resident on one CU at once: the
-// runtime's occupancy figure, capped by 160 KiB of LDS in 1-KiB allocation granules
-// (MI355X; the runtime figure alone over-counted k_snappy_enc: 12 where 11 fit, and the
-// 12th wave of each CU then ran after the others, +38 % time).  `fallback` if the queries fail.
+// runtime's occupancy figure, capped by 160 KiB of LDS in 2-KiB allocation granules
+// (MI355X, measured: the runtime figure alone over-counted k_snappy_enc -- 12 where 11
+// fit, the 12th wave of each CU then ran after the others, +38 % time -- and a 12.5-KiB
+// variant that 1-KiB granules would put at 12 per CU ran 1.54x slower, as 11 would).
+// `fallback` if the queries fail.
 inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback) {
     int b = 0;
     hipFuncAttributes fa;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block, 0) != hipSuccess || b <= 0 ||
         hipFuncGetAttributes(&fa, kernel) != hipSuccess)
         return fallback;
-    const size_t lds = (fa.sharedSizeBytes + 1023) & ~(size_t)1023;
+    const size_t lds = (fa.sharedSizeBytes + 2047) & ~(size_t)2047;
     if (lds) {
         const int by_lds = (int)((160u * 1024u) / lds);
         if (by_lds < b) b = by_lds;

@@ -25,6 +25,9 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_STAGE16
 #define BHG_SE_STAGE16 1  // measured: C4 30.7 vs 30.0 GiB/s (u16 table: 28.1 at 7 waves, 26.5 at 12)
 #endif
+#ifndef BHG_SE_DCNT
+#define BHG_SE_DCNT 256  // dwords of byte counters for the in-batch duplicate check (4 buckets each)
+#endif
 #ifndef BHG_SE_WAVES
 #define BHG_SE_WAVES 7
 #endif
@@ -164,7 +167,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint32_t h = se_hash(u, shift) & tmask;
             // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
             // of h mod 1024, one byte per bucket (<= 64 adds per byte)
-            const uint32_t slot = (h >> 2) & 255u, sh8 = 8 * (h & 3);
+            const uint32_t slot = (h >> 2) & (BHG_SE_DCNT - 1u), sh8 = 8 * (h & 3);
             atomicAdd(&dcnt[slot], valid ? 1u << sh8 : 0u);  // unconditional: no exec-mask branch
             wsync();
             const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
@@ -346,9 +349,9 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                                                    uint16_t *__restrict__ gtables) {
     __shared__ __attribute__((aligned(16))) uint8_t in[SE_CAP + 16];
     __shared__ __attribute__((aligned(16))) se_tab_t tab[SE_TAB];
-    __shared__ uint32_t dcnt[256];
+    __shared__ uint32_t dcnt[BHG_SE_DCNT];
     const uint32_t lane = threadIdx.x;
-    for (uint32_t j = lane; j < 256; j += 64) dcnt[j] = 0;
+    for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
     LaneSkip F;
 #pragma unroll
     for (uint32_t j = 0; j < 16; j++) {
