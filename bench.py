@@ -3,11 +3,18 @@
 
 One "step" = one pass of the hot path (bhg_decode_batch: CRC-32C verify
 against the writer's CRCs + readRecord validation + KV-record decode + FNV-1)
-over one batch of 1M synthetic blocks already resident in HBM
-(BASELINE.json configs[1]).  N GPUs (torch.distributed run, one rank per GPU)
-each decode their own tables: weak scaling, no data-path collective.  Rank 0
-prints one JSON line.  --config c5 is the fixed 25 GB corpus (184 tables x
-124,738 blocks) split round-robin by table over the N GPUs: strong scaling.
+over one batch of synthetic blocks already resident in HBM.
+
+  N = 1 (default): BASELINE.json configs[1], 1M blocks.  Nested: `strong_c5`,
+        the fixed 25 GB corpus (configs[4], 184 tables x 124,738 blocks) on this
+        one GPU -- the base of the strong-scaling curve -- and `c1` (configs[0],
+        100k blocks on the host CPU).
+  N > 1: `bench.py --gpus N` starts N rank processes itself when no launcher
+        did (torch.distributed.run works too); the line is the same 25 GB corpus
+        with table t decoded by rank t mod N (strong scaling: value = corpus
+        bytes / max-over-ranks time), RCCL only for the final reduction.
+        Nested: `weak_c2`, 1M blocks per GPU (weak scaling).
+  --config c1/c3/c4/c5/...: the other BASELINE configs and rows (see --help).
 
 Extra legs (N=1, rank 0, outside the timed region):
   * cpu_baseline -- the C restatement (oracle/) on the host cores, bounded sample:
@@ -51,8 +58,11 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--codec", default="none", choices=["none", "snappy"], help="c5 only")
     ap.add_argument("--c5-tables", type=int, default=184, help="c5 corpus size in 128 MiB tables")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "scan", "scanmix", "get", "indexcrc"],
-                    help="c2: uncompressed decode (BASELINE metric); c3: snappy decode; c4: encode; "
+    ap.add_argument("--no-c5", action="store_true", help="N=1: skip the nested strong_c5 record")
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "scan", "scanmix", "get",
+                                                       "indexcrc"],
+                    help="c1: 100k blocks on the host CPU; c2: uncompressed decode (BASELINE metric; at N > 1 "
+                         "the line is the C5 strong-scaling corpus); c3: snappy decode; c4: encode; "
                          "c5: 25 GB corpus sharded round-robin by table over the GPUs (strong scaling); "
                          "scan/scanmix: table data-region scan over uniform / mixed-length tables; "
                          "get: batched Bithash.Get (HashIndex + conflict SeekGE + readData) over full tables; "
@@ -132,11 +142,60 @@ def dist_sum_(t, world):
             t.copy_(h)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` with no outer launcher: start N rank processes of this
+    same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env), one per
+    GPU, and exit with the worst exit code.  This process never touches the GPU
+    (no HIP call happens before the children start), and the children are
+    started, not exec'd."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BHG_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        if failed:   # one rank died: the others would wait in a collective forever
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                try:
+                    rcs[r] = p.wait(30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    rcs[r] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE %d" % (a.gpus, world), file=sys.stderr)
+        sys.exit(2)
     import torch.distributed as dist
     global BACKEND
     BACKEND = a.backend
@@ -175,7 +234,37 @@ def run(a, world, rank, local, dev, codec):
         return run_indexcrc(a, world, rank, local, dev, codec)
     if a.config == "c5":
         return run_c5(a, world, rank, local, dev, codec)
-    import torch.distributed as dist
+    if a.config == "c1":
+        return run_c1(a, world, rank, local, dev, codec)
+    if world > 1:
+        # N > 1: the fixed 25 GB corpus split by table over the N GPUs (strong scaling), with
+        # the per-GPU C2 batch (weak scaling) nested
+        res = c5_measure(a, world, rank, local, dev, codec, "none", with_cpu=False)
+        torch.cuda.empty_cache()
+        weak = c2_measure(a, world, rank, local, dev, codec, with_extras=False)
+        if rank == 0:
+            res["weak_c2"] = {k: weak[k] for k in ("value", "unit", "ms_per_step", "scaling", "roofline",
+                                                   "status_ok_blocks", "valid", "digest_all_ranks")}
+            res["weak_c2"]["workload"] = weak["config"]["workload"]
+            res["weak_c2"]["per_gpu_GiBps"] = round(weak["value"] / world, 3)
+            print(json.dumps(res), flush=True)
+        return
+    out = c2_measure(a, world, rank, local, dev, codec, with_extras=True)
+    if not a.no_c5:
+        # the same fixed-corpus C5 measurement the N > 1 lines report, at N = 1: the base of the strong-scaling curve
+        torch.cuda.empty_cache()
+        s = c5_measure(a, world, rank, local, dev, codec, "none", with_cpu=False)
+        out["strong_c5"] = {k: s[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "per_gpu_GiBps",
+                                              "roofline", "status_ok_blocks", "valid", "digest_all_ranks",
+                                              "ranks_seen")}
+        out["strong_c5"]["workload"] = s["config"]["workload"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def c2_measure(a, world, rank, local, dev, codec, with_extras):
+    """BASELINE configs[1] on this rank's GPU: 1M blocks of its own tables,
+    CRC-verify + record decode, K timed steps.  Returns the bench line (dict)."""
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import handles_tensor
     n = a.blocks
@@ -272,7 +361,7 @@ def run(a, world, rank, local, dev, codec):
         "digest_all_ranks": "%016x" % digest_all,
     }
 
-    if rank == 0 and world == 1 and not a.no_e2e:
+    if rank == 0 and world == 1 and with_extras and not a.no_e2e:
         # end-to-end: host src -> H2D -> kernel -> D2H descriptors (bhg_decode_batch_host; handles are
         # sorted, so the 64 MiB-chunk 3-stream pipeline runs).  Pageable first, then the same buffer
         # page-locked with bhg_host_register (an mmap'd table file pinned once per mapping).
@@ -305,7 +394,7 @@ def run(a, world, rank, local, dev, codec):
     else:
         host_src = None
 
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if rank == 0 and world == 1 and with_extras and not a.no_cpu:
         from oracle import oracle as O
         if host_src is None:
             host_src = src_t.cpu().numpy()
@@ -355,7 +444,56 @@ def run(a, world, rank, local, dev, codec):
                                         "cache, as Reader.readData's ReadAt (reader.go:251)"}}
         out["parity_vs_restatement"] = "bit-exact" if parity else "MISMATCH"
         out["valid"] = bool(out["valid"] and parity)
+        out["c1"] = c1_baseline(host_src, h, exp_host, L)
+    return out
 
+
+def c1_baseline(host_src, h, exp_host, L, m=100_000):
+    """BASELINE configs[0] (C1): the reader on the host CPU over 100k uncompressed
+    blocks -- the C restatement of readData/readRecord + CRC verify + FNV-1
+    (1 thread and every usable core), plumbing only, no GPU."""
+    from oracle import oracle as O
+    hs, es = h[:m], exp_host[:m]
+    res = {}
+    for name, thr in (("one_thread", 1), ("all_cores", usable_cores())):
+        reps, t = 0, time.perf_counter()
+        while True:
+            O.decode_batch(host_src, hs, expected_crc=es, nthreads=thr)
+            reps += 1
+            if time.perf_counter() - t >= 1.0:
+                break
+        res[name] = round(reps * m * L / (time.perf_counter() - t) / 2 ** 30, 3)
+    return {"workload": "BASELINE configs[0]: %d uncompressed blocks (32B/1KB) decoded on the host" % m,
+            "unit": "GiB/s", "value": res["one_thread"], "one_thread": res["one_thread"],
+            "all_cores": res["all_cores"], "cores": usable_cores(), "kind": "port", "cpu": cpu_info()}
+
+
+def run_c1(a, world, rank, local, dev, codec):
+    """BASELINE configs[0] as its own line: C1 on the host (1 thread = value, and
+    every core), the GPU decode of the same 100k blocks beside it."""
+    from bitalosdb_amd import synth
+    from bitalosdb_amd.codec import handles_tensor
+    n = 100_000
+    src_t, h, meta = synth.uniform_tables(n, device=dev, seed=synth.SEED)
+    h_t = handles_tensor(h, dev)
+    exp_crc = codec.crc_batch(src_t, h_t, n)
+    desc_t = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    el, kms = _timed(a, dev, lambda: codec.decode_batch(src_t, src_t.numel(), h_t, n, expected_crc=exp_crc,
+                                                        out_desc=desc_t))
+    host = src_t.cpu().numpy()
+    c1 = c1_baseline(host, h, exp_crc.cpu().numpy().view(np.uint32), meta["rec_len"], m=n)
+    d = desc_t.cpu().numpy().view(DESC_DT)
+    from oracle import oracle as O
+    e, _, _ = O.decode_batch(host, h, expected_crc=exp_crc.cpu().numpy().view(np.uint32), nthreads=usable_cores())
+    out = {"metric": "GiB/s bithash blocks decoded on the host CPU (reference reader restated), 100k blocks",
+           "value": c1["value"], "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(n * meta["rec_len"] / (c1["value"] * 2 ** 30) * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": c1["workload"]}, "cpu": c1,
+           "gpu_same_blocks": {"value": round(n * meta["rec_len"] * a.steps / el / 2 ** 30, 3), "unit": "GiB/s",
+                               "step_event_ms": round(kms, 4)},
+           "parity_vs_restatement": "bit-exact" if all(np.array_equal(e[f], d[f]) for f in DESC_DT.names)
+           else "MISMATCH"}
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -495,23 +633,39 @@ def run_c4(a, world, rank, local, dev, codec):
                        "note": "k_snappy_enc is latency bound (DESIGN.md 4.3); snappy scratch traffic excluded"}
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
-        # bounded sample: the first 20k pairs, single thread (the restated writer is serial)
-        m = min(n, 20000)
-        vo = val_off.cpu().numpy()
+        vo = val_off.cpu().numpy().astype(np.uint64)
         vb = vals.cpu().numpy()
         kb = keys.cpu().numpy()
+        ko = key_off.cpu().numpy().astype(np.uint64)
+        trs = tr.cpu().numpy().astype(np.uint64)
+        # parity on the first 20k pairs (one restated writer, reference-definition CRC)
+        m = min(n, 20000)
         ks = [kb[32 * i:32 * i + 32].tobytes() for i in range(m)]
         vs = [vb[vo[i]:vo[i + 1]].tobytes() for i in range(m)]
-        trs = tr[:m].cpu().numpy()
-        t = time.perf_counter()
-        exp = O.encode_batch(ks, trs, vs, codec=1, file_nums=list(range(1, 100)))
-        cs = time.perf_counter() - t
+        exp = O.encode_batch(ks, trs[:m], vs, codec=1, file_nums=list(range(1, 100)))
         got_out = out_t.cpu().numpy()
         par = got_out[:len(exp["out"])].tobytes() == exp["out"].tobytes()
-        res["cpu_baseline"] = {"value": round(float(sum(len(v) for v in vs) + 32 * m) / cs / 2 ** 30, 3),
-                               "unit": "GiB/s", "cores": 1, "kind": "port",
-                               "sample": "first %d pairs, restated BithashWriter.Add + golang/snappy Encode, 1 thread (%s)"
-                                         % (m, cpu_info())}
+        # baseline: every usable core (independent writers over contiguous pair ranges, all n pairs,
+        # repeated for ~cpu_seconds / 2), and 1 thread over the first 100k pairs
+        thr = usable_cores()
+        reps, t = 0, time.perf_counter()
+        while True:
+            O.encode_batch_mt(kb, ko, trs, vb, vo, n, 1, 128 << 20, thr)
+            reps += 1
+            if time.perf_counter() - t >= a.cpu_seconds / 2:
+                break
+        cs = time.perf_counter() - t
+        m1 = min(n, 100_000)
+        t = time.perf_counter()
+        O.encode_batch_mt(kb, ko, trs, vb, vo, m1, 1, 128 << 20, 1)
+        c1s = time.perf_counter() - t
+        raw1 = float(vo[m1] - vo[0]) + 32.0 * m1
+        res["cpu_baseline"] = {"value": round(raw * reps / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": thr,
+                               "kind": "port", "one_thread": round(raw1 / c1s / 2 ** 30, 3),
+                               "sample": "restated BithashWriter.Add + golang/snappy Encode + FNV-1 + masked CRC-32C "
+                                         "(SSE4.2): all %d pairs, %d passes in %.1f s on %d threads = every usable "
+                                         "core, one writer per contiguous pair range; one_thread: the first %d "
+                                         "pairs on 1 thread (%s)" % (n, reps, cs, thr, m1, cpu_info())}
         res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -520,43 +674,13 @@ def run_c4(a, world, rank, local, dev, codec):
 C5_RECORDS_PER_TABLE = 124_738      # 128 MiB / 1076 B, the add that crosses the limit included
 
 
-def _c5_snappy_tables(codec, owned, R, dev, seed):
-    """The owned tables of the C5 corpus in the snappy variant: table t's
-    R values (SURVEY §8d C3 generator, seeded per table) encoded on the GPU
-    into one table file data region (fileNum 1 + t, seqNums t*R+1..).
-    Returns (src, handles HANDLE_DT, expected CRCs int32 tensor, raw value bytes)."""
-    from bitalosdb_amd import synth
-    from bitalosdb_amd.codec import EncodeBuffers, HANDLE_DT
-    parts, hs, crcs = [], [], []
-    base, raw = 0, 0
-    for t in owned:
-        ts = synth.table_seed(seed, t)
-        keys = synth.keys_gpu(R, device=dev, seed=ts).reshape(-1).contiguous()
-        key_off = torch.arange(0, (R + 1) * 32, 32, dtype=torch.int64, device=dev)
-        tr = ((torch.arange(t * R + 1, (t + 1) * R + 1, dtype=torch.int64, device=dev)) << 8) | 1
-        vals = synth.compressible_values_gpu(R, 1024, device=dev, seed=ts + 1).reshape(-1).contiguous()
-        val_off = torch.arange(0, (R + 1) * 1024, 1024, dtype=torch.int64, device=dev)
-        out = torch.empty(R * 64 + vals.numel() * 7 // 6 + 64, dtype=torch.uint8, device=dev)
-        bufs = EncodeBuffers(R, 1, dev)
-        fns = torch.tensor([1 + t], dtype=torch.int32, device=dev)
-        codec.encode_batch(keys, key_off, tr, vals, val_off, R, 1, fns, 1, 0, 1 << 30, out, bufs,
-                           vals_len=vals.numel())
-        codec.sync()
-        size = int(bufs.table_size[0].item())
-        parts.append(out[:size + 12].clone())
-        parts[-1][size:] = 0                               # writeData's empty record header
-        h = np.zeros(R, dtype=HANDLE_DT)
-        h["offset"] = bufs.pos.cpu().numpy().view(np.uint64) + np.uint64(base)
-        h["length"] = bufs.bh_len.cpu().numpy().view(np.uint32)
-        hs.append(h)
-        crcs.append(bufs.crc.clone())
-        base += size + 12
-        raw += vals.numel()
-        del keys, vals, out, bufs
-    return torch.cat(parts), np.concatenate(hs), torch.cat(crcs), raw
-
-
 def run_c5(a, world, rank, local, dev, codec):
+    out = c5_measure(a, world, rank, local, dev, codec, a.codec, with_cpu=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
     """BASELINE configs[4]: a fixed 25 GB corpus of bithash table files (184
     tables x 124,738 blocks of 32 B key / 1 KiB value), table t decoded by
     rank t mod N (round-robin by table file).  Each rank decodes
@@ -569,10 +693,10 @@ def run_c5(a, world, rank, local, dev, codec):
     from bitalosdb_amd.codec import handles_tensor
     T, R = a.c5_tables, C5_RECORDS_PER_TABLE
     owned = shard.owned_tables(T, world, rank)
-    snappy = a.codec == "snappy"
+    snappy = codec_name == "snappy"
     t_build = time.perf_counter()
     if snappy:
-        src_t, h, exp_crc, raw = _c5_snappy_tables(codec, owned, R, dev, synth.SEED)
+        src_t, h, exp_crc, raw = synth.table_set_snappy(codec, owned, R, device=dev, seed=synth.SEED)
     else:
         src_t, h, meta = synth.table_set(owned, R, device=dev, seed=synth.SEED, first_file_num=1)
         raw = len(h) * 1024
@@ -622,6 +746,8 @@ def run_c5(a, world, rank, local, dev, codec):
     dt = torch.tensor([disk, raw], dtype=torch.float64, device=dev)
     dist_sum_(dt, world)
     disk_total, raw_total = float(dt[0].item()), float(dt[1].item())
+    ranks = torch.ones(1, dtype=torch.int64, device=dev)
+    dist_sum_(ranks, world)          # the world size the collective backend (RCCL for N > 1) reports
     value = disk_total * a.steps / el_max / 2 ** 30
     # per-GPU roofline of this rank's step: algorithmic bytes (handle + record + descriptor + expected CRC,
     # + decoded value bytes written for snappy) over the event-timed step
@@ -637,18 +763,19 @@ def run_c5(a, world, rank, local, dev, codec):
         "config": {"workload": "BASELINE configs[4]: %d tables x %d blocks (%.2f GB on disk), table t -> rank t "
                                "mod %d, CRC-verify + record decode%s" % (T, R, disk_total / 1e9, world,
                                                                         " + snappy decompress" if snappy else ""),
-                   "codec": a.codec, "tables": T, "tables_this_rank": len(owned), "blocks_total": int(n_total),
+                   "codec": codec_name, "tables": T, "tables_this_rank": len(owned), "blocks_total": int(n_total),
                    "parallelism": "table-sharded x%d" % world, "corpus_build_s": round(build_s, 2)},
         "per_gpu_GiBps": round(value / world, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "scope": "rank 0, per GPU",
                      "step_avg_ms": round(step_ms, 4)},
         "status_ok_blocks": int(ok_total), "valid": bool(ok_total == n_total == T * R),
-        "digest_all_ranks": "%016x" % digest_all,
+        "digest_all_ranks": "%016x" % digest_all, "ranks_seen": int(ranks.item()),
+        "backend": BACKEND if world > 1 else None,
     }
     if snappy:
         out["decoded_GiBps"] = round(raw_total * a.steps / el_max / 2 ** 30, 3)
-    if rank == 0 and world == 1 and not a.no_cpu and n:
+    if rank == 0 and world == 1 and with_cpu and not a.no_cpu and n:
         from oracle import oracle as O
         # parity + baseline on a bounded sample: the first table (the restatement decodes it bit for bit)
         first = np.nonzero(h["offset"] >= 0)[0][:R]
@@ -674,8 +801,7 @@ def run_c5(a, world, rank, local, dev, codec):
                                                          "%d threads (%s)" % (R, hi - lo, reps, threads, cpu_info())}
         out["parity_table0_vs_restatement"] = "bit-exact" if par else "MISMATCH"
         out["valid"] = bool(out["valid"] and par)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    return out
 
 
 def run_scan(a, world, rank, local, dev, codec):

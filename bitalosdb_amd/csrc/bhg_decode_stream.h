@@ -212,7 +212,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         auto locate = [&](uint32_t ps) {
             PassIn pi;
             if (KO & 256) {  // probe addressing (lab): the tile's first record start + 8 KB per pass
-                const uint64_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)p) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+                const uint64_t b0 = readfirstlane_u64(p);
                 pi.act = ps * 64 + lane < total;
                 pi.head = false;
                 pi.padr = 0;

@@ -43,6 +43,22 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 // vmcnt(0) after the stores, exposing a full store round trip per tile.
 __device__ __forceinline__ void wait_loads_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// Lane `src`'s 64-bit value, wave-uniform (two v_readlane_b32), and lane 0's
+// (v_readfirstlane_b32).  The builtins return int: each half goes through
+// uint32_t before widening, or a low word with bit 31 set sign-extends into the
+// high word -- the cause of round 2's intermittent snappy-decoder faults.
+// tests/test_addr_host.py compiles these for the host and checks that case.
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 __device__ __forceinline__ uint32_t crc_table_entry(uint32_t i) {
     uint32_t c = i;
 #pragma unroll

@@ -395,8 +395,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     // loads until the next dump.  (The launcher sends src_len < 64 elsewhere.)
     auto chunk_addr = [&](const SlInfo &I, int b, uint32_t &clb) -> uint64_t {
         clb = __builtin_amdgcn_readlane(I.mode == SL_LDS ? I.clen : 0u, b);
-        const uint64_t cpb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)I.cp, b) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(I.cp >> 32), b) << 32);
+        const uint64_t cpb = readlane_u64(I.cp, b);
         return 16 * lane < clb ? cpb + 16 * lane : base;
     };
     auto prefetch = [&](const SlInfo &I) {
@@ -452,9 +451,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             for (int b = 0; b < BPW; b++) {
                 const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
                 if (16 * lane < dlb) {
-                    const uint64_t ob = (uint64_t)out_vals +
-                                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)cur.o0, b) |
-                                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(cur.o0 >> 32), b) << 32));
+                    const uint64_t ob = (uint64_t)out_vals + readlane_u64(cur.o0, b);
                     st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + 16 * lane),
                               ob + dlb);
                 }

@@ -114,6 +114,49 @@ def table_set(table_ids, records_per_table, key_len=32, val_len=1024, device="cu
     return src, h, meta
 
 
+def table_set_snappy(codec, table_ids, records_per_table, device="cuda", seed=SEED, val_len=1024):
+    """The snappy variant of table_set(): table t's records_per_table values
+    (compressible_values_gpu, seeded per table) encoded on the GPU by
+    bhg_encode_batch (SnappyCompressor, fileNum 1 + t, seqNums t*R+1..) into one
+    data region + 12-byte terminator each, concatenated in the order given.
+    Returns (src uint8 tensor, handles HANDLE_DT, writer CRCs int32 tensor,
+    raw value bytes)."""
+    from ._lib import HANDLE_DT
+    from .codec import EncodeBuffers
+    device = torch.device(device)
+    R = int(records_per_table)
+    parts, hs, crcs = [], [], []
+    base, raw = 0, 0
+    for t in table_ids:
+        ts = table_seed(seed, t)
+        keys = keys_gpu(R, device=device, seed=ts).reshape(-1).contiguous()
+        key_off = torch.arange(0, (R + 1) * 32, 32, dtype=torch.int64, device=device)
+        tr = (torch.arange(t * R + 1, (t + 1) * R + 1, dtype=torch.int64, device=device) << 8) | 1
+        vals = compressible_values_gpu(R, val_len, device=device, seed=ts + 1).reshape(-1).contiguous()
+        val_off = torch.arange(0, (R + 1) * val_len, val_len, dtype=torch.int64, device=device)
+        out = torch.empty(R * 64 + vals.numel() * 7 // 6 + 64, dtype=torch.uint8, device=device)
+        bufs = EncodeBuffers(R, 1, device)
+        fns = torch.tensor([1 + t], dtype=torch.int32, device=device)
+        codec.encode_batch(keys, key_off, tr, vals, val_off, R, 1, fns, 1, 0, 1 << 30, out, bufs,
+                           vals_len=vals.numel())
+        codec.sync()
+        size = int(bufs.table_size[0].item())
+        parts.append(out[:size + 12].clone())
+        parts[-1][size:] = 0                               # writeData's empty record header
+        h = np.zeros(R, dtype=HANDLE_DT)
+        h["offset"] = bufs.pos.cpu().numpy().view(np.uint64) + np.uint64(base)
+        h["length"] = bufs.bh_len.cpu().numpy().view(np.uint32)
+        hs.append(h)
+        crcs.append(bufs.crc.clone())
+        base += size + 12
+        raw += vals.numel()
+        del keys, vals, out, bufs
+    if not parts:
+        return (torch.zeros(0, dtype=torch.uint8, device=device), np.zeros(0, dtype=HANDLE_DT),
+                torch.zeros(0, dtype=torch.int32, device=device), 0)
+    return torch.cat(parts), np.concatenate(hs), torch.cat(crcs), raw
+
+
 def compressible_values(rng, n_vals, val_len, dict_size=4096, fresh=0.2):
     """Values of tokens (4-64 B) drawn from a seeded dictionary, ~20 % fresh
     random bytes -- the SURVEY §8d C3 generator (numpy, host)."""

@@ -432,12 +432,93 @@ void bho_decode_sizes(const uint8_t *src, uint64_t src_len, const bho_handle *h,
 #define MAX_VALUE_SIZE (256u << 20)
 #define DATA_MAX_SIZE (0xFFFFFFFFu - (256u << 20))
 
+static int encode_seq(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                      const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                      const uint32_t *file_nums, int max_tables, uint32_t init_size, uint64_t table_max,
+                      uint8_t *out, uint64_t *out_len, uint64_t *out_pos, uint32_t *out_bh_off,
+                      uint32_t *out_bh_len, uint32_t *out_table, uint32_t *fnv, uint32_t *crc,
+                      uint32_t *status, uint32_t *out_table_start, int fast);
+
 int bho_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
                      const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
                      const uint32_t *file_nums, int max_tables, uint32_t init_size, uint64_t table_max,
                      uint8_t *out, uint64_t *out_len, uint64_t *out_pos, uint32_t *out_bh_off,
                      uint32_t *out_bh_len, uint32_t *out_table, uint32_t *fnv, uint32_t *crc,
                      uint32_t *status, uint32_t *out_table_start) {
+    return encode_seq(keys, key_off, trailers, vals, val_off, n, codec, file_nums, max_tables, init_size,
+                      table_max, out, out_len, out_pos, out_bh_off, out_bh_len, out_table, fnv, crc, status,
+                      out_table_start, 0);
+}
+
+/* CPU baseline of the encode path on many cores (reported only): nthreads
+ * independent BithashWriters (the reference serialises Adds per Writer,
+ * writers run concurrently), thread t taking the contiguous pair range
+ * [n t / T, n (t+1) / T) -- golang/snappy Encode + FNV-1 + record pack +
+ * masked CRC-32C (SSE4.2) per pair, 128 MiB table splits.  Returns the total
+ * bytes written, or 0 on allocation failure. */
+typedef struct {
+    const uint8_t *keys; const uint64_t *key_off; const uint64_t *trailers; const uint8_t *vals;
+    const uint64_t *val_off; uint32_t lo, hi; int codec; uint64_t table_max; uint64_t written; int fail;
+} enc_job;
+
+static void *enc_worker(void *arg) {
+    enc_job *j = (enc_job *)arg;
+    uint32_t m = j->hi - j->lo;
+    size_t cap = 1;
+    for (uint32_t i = j->lo; i < j->hi; i++)
+        cap += 20 + (size_t)(j->key_off[i + 1] - j->key_off[i]) +
+               (size_t)bho_snappy_max_encoded_len((int64_t)(j->val_off[i + 1] - j->val_off[i])) + 16;
+    uint8_t *out = (uint8_t *)malloc(cap);
+    uint64_t *pos = (uint64_t *)malloc(((size_t)m + 1) * 8);
+    uint32_t *u32 = (uint32_t *)malloc(((size_t)m + 1) * 4 * 6 + 4096 * 8);
+    if (!out || !pos || !u32) { j->fail = 1; free(out); free(pos); free(u32); return NULL; }
+    uint32_t *fns = u32 + ((size_t)m + 1) * 6, *tstart = fns + 4096;
+    for (uint32_t t = 0; t < 4096; t++) fns[t] = t + 1;
+    uint64_t len = 0;
+    /* offsets are absolute: pass the range's own base pointers */
+    const uint64_t *ko = j->key_off + j->lo, *vo = j->val_off + j->lo;
+    uint64_t *kor = (uint64_t *)malloc(((size_t)m + 1) * 16);
+    if (!kor) { j->fail = 1; free(out); free(pos); free(u32); return NULL; }
+    uint64_t *vor = kor + m + 1;
+    for (uint32_t i = 0; i <= m; i++) { kor[i] = ko[i] - ko[0]; vor[i] = vo[i] - vo[0]; }
+    size_t q = (size_t)m + 1;
+    int nt = encode_seq(j->keys + ko[0], kor, j->trailers + j->lo, j->vals + vo[0], vor, m, j->codec, fns, 4096, 0,
+                        j->table_max, out, &len, pos, u32, u32 + q, u32 + 2 * q, u32 + 3 * q, u32 + 4 * q,
+                        u32 + 5 * q, tstart, 1);
+    j->fail = nt < 0;
+    j->written = len;
+    free(kor); free(out); free(pos); free(u32);
+    return NULL;
+}
+
+uint64_t bho_encode_batch_mt(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                             const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                             uint64_t table_max, int nthreads) {
+    int nt = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+    pthread_t tid[256];
+    enc_job jobs[256];
+    for (int t = 0; t < nt; t++)
+        jobs[t] = (enc_job){keys, key_off, trailers, vals, val_off, (uint32_t)((uint64_t)n * t / nt),
+                            (uint32_t)((uint64_t)n * (t + 1) / nt), codec, table_max, 0, 0};
+    if (nt == 1) enc_worker(&jobs[0]);
+    else {
+        for (int t = 0; t < nt; t++) pthread_create(&tid[t], NULL, enc_worker, &jobs[t]);
+        for (int t = 0; t < nt; t++) pthread_join(tid[t], NULL);
+    }
+    uint64_t total = 0;
+    for (int t = 0; t < nt; t++) {
+        if (jobs[t].fail) return 0;
+        total += jobs[t].written;
+    }
+    return total;
+}
+
+static int encode_seq(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                      const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                      const uint32_t *file_nums, int max_tables, uint32_t init_size, uint64_t table_max,
+                      uint8_t *out, uint64_t *out_len, uint64_t *out_pos, uint32_t *out_bh_off,
+                      uint32_t *out_bh_len, uint32_t *out_table, uint32_t *fnv, uint32_t *crc,
+                      uint32_t *status, uint32_t *out_table_start, int fast) {
     int t = 0;
     uint32_t size = init_size;          /* meta.Size == currentOffset for a data-only writer */
     uint64_t pos = 0;
@@ -466,7 +547,7 @@ int bho_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint64_
         status[i] = BHO_OK;
         out_pos[i] = pos;
         out_bh_off[i] = size; out_bh_len[i] = (uint32_t)L;  /* BlockHandle{currentOffset, length} */
-        crc[i] = bho_crc_masked(out + pos, L);
+        crc[i] = fast ? crc_masked_fast(out + pos, L) : bho_crc_masked(out + pos, L);
         pos += L;
         size += (uint32_t)L;
         if ((uint64_t)size >= table_max) {                  /* maybeSplitTable: isWriteFull after add */

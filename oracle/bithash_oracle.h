@@ -101,6 +101,10 @@ void bho_decode_sizes(const uint8_t *src, uint64_t src_len, const bho_handle *h,
  * fnv[i], crc[i], status[i]; out_table_start[t] = first record of
  * table t; returns number of tables used (>=1) or -1 if max_tables
  * is too small. *out_len = bytes written. */
+/* reported-only CPU baseline: nthreads independent writers over contiguous pair ranges */
+uint64_t bho_encode_batch_mt(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
+                             const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
+                             uint64_t table_max, int nthreads);
 int bho_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint64_t *trailers,
                      const uint8_t *vals, const uint64_t *val_off, uint32_t n, int codec,
                      const uint32_t *file_nums, int max_tables, uint32_t init_size,

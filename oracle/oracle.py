@@ -64,6 +64,8 @@ def lib():
         L.bho_decode_sizes.argtypes = [P, U64, P, U32, P]
         L.bho_encode_batch.restype = I
         L.bho_encode_batch.argtypes = [P, P, P, P, P, U32, I, P, I, U32, U64, P, P, P, P, P, P, P, P, P, P]
+        L.bho_encode_batch_mt.restype = U64
+        L.bho_encode_batch_mt.argtypes = [P, P, P, P, P, U32, I, U64, I]
         L.bho_scan_region.restype = ctypes.c_int64
         L.bho_scan_region.argtypes = [P, U64, I, P, U64, ctypes.POINTER(U64)]
         _lib = L
@@ -220,6 +222,20 @@ def encode_batch(keys, trailers, values, codec=0, file_nums=(1,), init_size=0, t
         raise ValueError("not enough file numbers for the table splits")
     return dict(out=out[:out_len.value], pos=pos, bh_off=bh_off, bh_len=bh_len, table=tab, fnv=fnv,
                 crc=crc, status=st, table_start=tstart[:nt], ntables=nt)
+
+
+def encode_batch_mt(keys, key_off, trailers, vals, val_off, n, codec=1, table_max=128 << 20, nthreads=1):
+    """CPU baseline of the encode path (bho_encode_batch_mt): flat numpy keys /
+    values with u64 offsets[n+1]; nthreads independent writers over contiguous
+    pair ranges.  Returns the bytes written."""
+    kb, vb = _u8(keys), _u8(vals)
+    ko = np.ascontiguousarray(key_off, dtype=np.uint64)
+    vo = np.ascontiguousarray(val_off, dtype=np.uint64)
+    tr = np.ascontiguousarray(trailers, dtype=np.uint64)
+    w = lib().bho_encode_batch_mt(_ptr(kb), _ptr(ko), _ptr(tr), _ptr(vb), _ptr(vo), n, codec, table_max, nthreads)
+    if w == 0 and n:
+        raise MemoryError("bho_encode_batch_mt")
+    return w
 
 
 def scan_region(data, mode=0, max_records=None):

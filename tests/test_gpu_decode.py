@@ -242,6 +242,74 @@ def test_snappy_inplace_spill_and_oversize(codec):
     assert gvals[int(goff[0]):int(goff[1])].tobytes() == want
 
 
+def _view_with_bit31(nbytes, dev):
+    """A uint8 device view of nbytes whose address has bit 31 of its low word set
+    over its whole length (low word in [0x80000100, 0xFFFFFFFF])."""
+    assert nbytes < (1 << 30)
+    big = torch.empty((1 << 31) + 2 * nbytes + (1 << 20), dtype=torch.uint8, device=dev)
+    lo = big.data_ptr() & 0xFFFFFFFF
+    if 0x80000100 <= lo <= 0xFFFFFFFF - nbytes - 4096:
+        off = 0
+    elif lo < 0x80000100:
+        off = 0x80000100 - lo
+    else:
+        off = (1 << 32) - lo + 0x80000100
+    v = big[off:off + nbytes]
+    a = v.data_ptr()
+    assert (a & 0xFFFFFFFF) >= 0x80000000 and ((a + nbytes - 1) & 0xFFFFFFFF) >= 0x80000000
+    return big, v
+
+
+def test_snappy_addresses_with_bit31_set(codec):
+    """Round 2's intermittent fault, pinned: src and out_vals placed where the low
+    32 bits of every device address have bit 31 set, so a sign-extending
+    composition of a readlane'd address would fault or write elsewhere.  The
+    batch mixes slot-resident blocks (k_snappy_lds), in-place spill hand-overs
+    and oversize / incompressible blocks (k_snappy_rt)."""
+    from bitalosdb_amd.codec import handles_tensor
+    rng = random.Random(31)
+    body = bytes([0 << 2]) + b"x"
+    body += (bytes([(64 - 1) << 2 | 2]) + (1).to_bytes(2, "little")) * 10
+    body += bytes([(59 - 1) << 2 | 2]) + (1).to_bytes(2, "little")
+    body += (bytes([0 << 2 | 2]) + (7).to_bytes(2, "little")) * 324
+    spill = _uvarint(1024) + body
+    streams = []
+    for i in range(4000):
+        k = i % 5
+        if k == 0:
+            streams.append(spill)
+        elif k == 1:
+            streams.append(O.snappy_encode(rand_bytes(rng, 1024)))
+        elif k == 2:
+            streams.append(O.snappy_encode(compressible(rng, 2500)))
+        else:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([16, 700, 1024]))))
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"bit31-%d" % i, (i + 1) << 8 | 1, st, 5)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert (exp["status"] == 0).all()
+    total = int(eoff[-1])
+    dev = codec.device
+    with torch.cuda.stream(codec.stream):
+        big_s, src_t = _view_with_bit31(len(src), dev)
+        src_t.copy_(torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev))
+        big_v, vals_t = _view_with_bit31(total + 64, dev)
+        ht = handles_tensor(h, dev)
+        res = codec.decode_batch(src_t, len(src), ht, len(h), 1, out_vals=vals_t)
+        codec.sync()
+        got = res.desc_np()
+        gv = vals_t[:total].cpu().numpy()
+    assert_desc_equal(got, exp)
+    assert np.array_equal(res.val_off_np(), eoff)
+    assert gv.tobytes() == evals[:total].tobytes()
+    del big_s, big_v
+
+
 def test_known_answer_tables(codec):
     """K1 + K2 tables written by the restated writer, scanned, decoded on GPU."""
     rng = random.Random(9)
