@@ -158,12 +158,24 @@ def spawn_ranks(n):
     (no HIP call happens before the children start), and the children are
     started, not exec'd."""
     import subprocess
+    import threading
     port = _free_port()
     procs = []
+
+    def forward(pipe):   # rank 0's stdout: the JSON line to stdout, library chatter (gloo) to stderr
+        for line in iter(pipe.readline, b""):
+            (sys.stdout if line.lstrip().startswith(b"{") else sys.stderr).buffer.write(line)
+            (sys.stdout if line.lstrip().startswith(b"{") else sys.stderr).flush()
+
+    fwd = None
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BHG_BENCH_SPAWNED="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+        if r == 0:
+            fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+            fwd.start()
     rcs = [None] * n
     while any(rc is None for rc in rcs):
         for r, p in enumerate(procs):
@@ -182,6 +194,7 @@ def spawn_ranks(n):
                     rcs[r] = p.wait()
             break
         time.sleep(0.05)
+    fwd.join(30)
     bad = [rc for rc in rcs if rc != 0]
     return (bad[0] if bad[0] > 0 else 1) if bad else 0
 

@@ -292,7 +292,11 @@ __global__ __launch_bounds__(256) void k_enc_rawvals(const uint64_t *val_off, ui
 // inputs of each record read straight from its bytes -- what TableIterator
 // hands compactBithashFiles (table.go:358-395: ikey, stored value, header
 // fileNum).  A handle that is out of range or not a whole record
-// (12 + ikeySize + valueSize != length, ikeySize < 8) -> RECORD_NIL.
+// (12 + ikeySize + valueSize != length, ikeySize == 0) -> RECORD_NIL.  A
+// record with ikeySize 1..7 is what readKV returns it as (block2.go:38-55):
+// an empty UserKey and trailer InternalKeyKindInvalid (255), so AddIkey
+// re-writes it with ikeySize 8 -- the liveness filter decides, as in
+// compactBithashFiles.
 __global__ __launch_bounds__(256) void k_repack_prep(const uint8_t *src, uint64_t src_len, const bhg_handle *h,
                                                      uint32_t n, uint64_t *key_off, uint32_t *key_len,
                                                      uint64_t *trailers, uint64_t *vpos, uint64_t *vlen,
@@ -302,21 +306,23 @@ __global__ __launch_bounds__(256) void k_repack_prep(const uint8_t *src, uint64_
         const bhg_handle r = h[i];
         uint32_t st = BHG_ST_RECORD_NIL, k = 8, v = 0, fn = 0;
         uint64_t tr = 0;
-        if (r.length >= 20 && r.offset <= src_len && (uint64_t)r.length <= src_len - r.offset) {
+        uint32_t kl = 0;
+        if (r.length >= 13 && r.offset <= src_len && (uint64_t)r.length <= src_len - r.offset) {
             const uint64_t p = base + r.offset;
             k = ldu32(p, end);
             v = ldu32(p + 4, end);
             fn = ldu32(p + 8, end);
-            if (k >= 8 && 12ull + k + v == r.length) {
+            if (k >= 1 && 12ull + k + v == r.length) {
                 st = BHG_ST_OK;
-                tr = ldu64(p + 12 + k - 8, end);
+                kl = k >= 8 ? k - 8 : 0u;
+                tr = k >= 8 ? ldu64(p + 12 + k - 8, end) : 255ull;  // InternalKeyKindInvalid
             } else {
                 k = 8;
                 v = 0;
             }
         }
         key_off[i] = r.offset + 12;
-        key_len[i] = k - 8;
+        key_len[i] = kl;
         trailers[i] = tr;
         vpos[i] = r.offset + 12 + k;
         vlen[i] = v;

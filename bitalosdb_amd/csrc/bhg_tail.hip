@@ -20,6 +20,9 @@
 //   k_tail_heads   lane/position: run-head flags -> scan -> run index
 //   k_tail_runs    lane/run: run position, key, length, conflict flag
 //   k_tail_keep    lane/position: last occurrence of its key in a conflict run
+//   k_tail_dedupe  lane/kept position: a key kept by two runs of one table
+//                  (the caller passed one key under two khash values) stays
+//                  only where conflictKeys[key] was assigned last
 //                  -> scan -> conflict list (sorted by table)
 //   k_tail_tables  lane/table: run range, conflict range, tail size bound
 //                  -> scan -> tail_off
@@ -68,6 +71,7 @@ struct TailArgs {
     uint64_t *run_key;              // n
     uint8_t *run_conf;              // n
     uint64_t *keep, *kpos;          // n+1
+    uint32_t *kat;                  // n: when updateHash last assigned conflictKeys[key] from this run
     uint32_t *clist, *cord;         // n
     uint64_t *csz;                  // n+1: conflict entry sizes -> offsets
     uint32_t *tab_run, *tab_c;      // ntables+1
@@ -211,6 +215,25 @@ __global__ __launch_bounds__(256) void k_tail_keep(TailArgs a) {
                 if (keep) {  // blockWriter entry bound: 3 varints + ikey + 8-B handle + a restart slot
                     atomicAdd(reinterpret_cast<unsigned long long *>(a.cbound + (k >> 32)),
                               (unsigned long long)(15 + kl + 8 + 8 + 4));
+                    // updateHash (writer.go:285-310) assigns conflictKeys[key] at every add of the key
+                    // once the run conflicts, and the run's first key once more at the add that makes
+                    // it conflict (conflictKeys[ih.userKey] = ih.bh): the assignment time is the
+                    // later of this last add and, for the first key, that add
+                    uint32_t at = a.idx_s[j];
+                    const uint32_t p0 = a.run_pos[r];
+                    uint64_t k0; uint32_t l0;
+                    rec_key(a, a.idx_s[p0], k0, l0);
+                    if (key_eq(kp, kl, k0, l0)) {
+                        uint32_t q = p0 + 1;
+                        for (; q < e; q++) {
+                            uint64_t kq; uint32_t lq;
+                            rec_key(a, a.idx_s[q], kq, lq);
+                            if (!key_eq(k0, l0, kq, lq)) break;
+                        }
+                        const uint32_t tc = a.idx_s[q < e ? q : e - 1];
+                        at = at > tc ? at : tc;
+                    }
+                    a.kat[j] = at;
                 }
             }
         }
@@ -218,9 +241,33 @@ __global__ __launch_bounds__(256) void k_tail_keep(TailArgs a) {
     }
 }
 
+// conflictKeys is one map per table, keyed by user key: a key kept by two runs (two khash
+// values for one key, possible through AddIkey) keeps the run that assigned it last.  Without
+// this the conflict list would hold a key twice and the rank permutation would break.
+__global__ __launch_bounds__(256) void k_tail_dedupe(TailArgs a) {
+    GRID_LOOP(j, a.n) {
+        uint64_t f = a.keep[j];
+        if (f) {
+            const uint64_t t = a.sk_s[j] >> 32;
+            const uint32_t p0 = lower_bound(0, a.n, t << 32, [&](uint32_t q) { return a.sk_s[q]; });
+            const uint32_t p1 = lower_bound(p0, a.n, (t + 1) << 32, [&](uint32_t q) { return a.sk_s[q]; });
+            uint64_t kp; uint32_t kl;
+            rec_key(a, a.idx_s[j], kp, kl);
+            const uint32_t at = a.kat[j];
+            for (uint32_t q = p0; q < p1 && f; q++) {
+                if (q == j || !a.keep[q] || a.kat[q] < at || (a.kat[q] == at && q < j)) continue;
+                uint64_t kq; uint32_t lq;
+                rec_key(a, a.idx_s[q], kq, lq);
+                if (key_eq(kp, kl, kq, lq)) f = 0;
+            }
+        }
+        a.kpos[j] = f;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_tail_clist(TailArgs a) {
     GRID_LOOP(j, a.n) {
-        if (a.keep[j]) a.clist[a.kpos[j]] = (uint32_t)j;
+        if (a.kpos[j + 1] != a.kpos[j]) a.clist[a.kpos[j]] = (uint32_t)j;
     }
 }
 
@@ -262,7 +309,7 @@ __global__ __launch_bounds__(256) void k_conf_rank(TailArgs a) {
             rec_key(a, a.idx_s[a.clist[f]], fp, fl);
             rank += key_lt(fp, fl, kp, kl);
         }
-        a.cord[c0 + rank] = (uint32_t)g;  // keys of a table are distinct: ranks are a permutation
+        a.cord[c0 + rank] = (uint32_t)g;  // keys of a table are distinct (k_tail_dedupe): ranks are a permutation
     }
 }
 
@@ -485,8 +532,8 @@ size_t tail_scratch_bytes(uint32_t n, uint32_t ntables) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t N = (size_t)n + 1, T = (size_t)ntables + 1;
     return al(sort_tmp) + 2 * al(N * 8) + 2 * al(N * 4) + 2 * al(N * 8) + 2 * al(N * 4) + al(N * 8) + al(N) +
-           2 * al(N * 8) + 2 * al(N * 4) + al(N * 8) + 2 * al(T * 4) + al(T * 8) + al(T * 8) + al(T * 16) +
-           al(T * 4) + al(scan_scratch_bytes(N)) + 24 * 256;
+           2 * al(N * 8) + al(N * 4) + 2 * al(N * 4) + al(N * 8) + 2 * al(T * 4) + al(T * 8) + al(T * 8) +
+           al(T * 16) + al(T * 4) + al(scan_scratch_bytes(N > T ? N : T)) + 24 * 256;
 }
 
 hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch) {
@@ -507,13 +554,13 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     a.head = (uint64_t *)take(N * 8); a.runidx = (uint64_t *)take(N * 8);
     a.run_pos = (uint32_t *)take(N * 4); a.run_len = (uint32_t *)take(N * 4);
     a.run_key = (uint64_t *)take(N * 8); a.run_conf = take(N);
-    a.keep = (uint64_t *)take(N * 8); a.kpos = (uint64_t *)take(N * 8);
+    a.keep = (uint64_t *)take(N * 8); a.kpos = (uint64_t *)take(N * 8); a.kat = (uint32_t *)take(N * 4);
     a.clist = (uint32_t *)take(N * 4); a.cord = (uint32_t *)take(N * 4);
     a.csz = (uint64_t *)take(N * 8);
     a.tab_run = (uint32_t *)take(TT * 4); a.tab_c = (uint32_t *)take(TT * 4);
     a.cbound = (uint64_t *)take(TT * 8); a.cinfo = (uint32_t *)take(TT * 8);
     a.crc_h = (bhg_handle *)take(TT * 16); a.crc = (uint32_t *)take(TT * 4);
-    void *scan_s = take(scan_scratch_bytes(N));
+    void *scan_s = take(scan_scratch_bytes(N > TT ? N : TT));  // also scans tail_off over the tables
 
     const uint32_t g = lane_grid(L, n ? n : 1, 256);
     e = hipMemsetAsync(a.cbound, 0, TT * 8, L.stream);
@@ -526,7 +573,8 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     if ((e = launch_exclusive_scan_u64(L, a.head, a.runidx, n, scan_s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_runs, dim3(g), dim3(256), 0, L.stream, a);
     hipLaunchKernelGGL(k_tail_keep, dim3(g), dim3(256), 0, L.stream, a);
-    if ((e = launch_exclusive_scan_u64(L, a.keep, a.kpos, n, scan_s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tail_dedupe, dim3(g), dim3(256), 0, L.stream, a);
+    if ((e = launch_exclusive_scan_u64(L, a.kpos, a.kpos, n, scan_s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_clist, dim3(g), dim3(256), 0, L.stream, a);
     hipLaunchKernelGGL(k_tail_tables, dim3(lane_grid(L, (uint64_t)nt + 1, 256)), dim3(256), 0, L.stream, a);
     if ((e = launch_exclusive_scan_u64(L, a.tail_off, a.tail_off, nt, scan_s)) != hipSuccess) return e;

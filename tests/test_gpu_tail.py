@@ -249,3 +249,76 @@ def test_rebuild_multi_table_roundtrip(codec):
     off, ln = off.cpu().numpy(), ln.cpu().numpy()
     for i in range(4):
         assert t[off[i]:off[i] + ln[i]].tobytes() == wants[i], i
+
+
+def _ikey_table(codec, keys, trs, vals, khash, fn=9):
+    """AddIkey over the batch with caller-given khash (bhg_encode_ikey_batch), then
+    writeTable (bhg_table_tail): one whole table file."""
+    n = len(keys)
+    res = codec.encode_ikey(keys, trs, vals, [fn] * n, khash=khash)
+    assert (res["status"] == 0).all()
+    assert np.array_equal(res["fnv"], np.asarray(khash, np.uint32))
+    bufs = res["bufs"]
+    with torch.cuda.stream(codec.stream):
+        tail, off, ln, stats = codec.table_tail(res["out_t"], bufs.rec, bufs.bh_off, bufs.fnv1, bufs.table,
+                                               bufs.status, n, 1, bufs.table_size)
+        codec.sync()
+    size = int(bufs.table_size[0].item())
+    t = tail.cpu().numpy()
+    return res["out"][:size].tobytes() + t[int(off[0]):int(off[0]) + int(ln[0])].tobytes(), stats
+
+
+def _oracle_ikey_table(keys, trs, vals, khash, fn=9):
+    w = T.Writer(fn, 1 << 40)
+    for k, tr, v, kh in zip(keys, trs, vals, khash):
+        w.add_ikey(k, tr, v, kh, fn)
+    w.write_table(True)
+    return bytes(w.file), w
+
+
+def test_tail_conflict_block_past_one_restart(codec):
+    """A conflict block of 41 keys (restart points at entries 0, 16, 32) whose keys
+    share long prefixes, so every entry between restarts is prefix-compressed:
+    all 41 under one khash, some re-added after the group turned conflicting."""
+    rng = random.Random(41)
+    keys = [b"shared/prefix/of/conflict/keys/%03d" % (i * 7 % 41) for i in range(41)]
+    keys += [keys[i] for i in (3, 17, 40, 0)]                     # re-adds: conflictKeys updated
+    keys += [b"other_%d" % i for i in range(30)]                  # ordinary index items
+    khash = [0xABCD1234] * 45 + [O.fnv32(k) for k in keys[45:]]
+    trs = [((i + 1) << 8) | 1 for i in range(len(keys))]
+    vals = [rb(rng, rng.choice([5, 100, 700])) for _ in keys]
+    got, stats = _ikey_table(codec, keys, trs, vals, khash)
+    exp, w = _oracle_ikey_table(keys, trs, vals, khash)
+    assert len(w.conflict_keys) == 41 and int(stats[0, 1]) == 41
+    assert got == exp
+    for k in (keys[0], keys[20], keys[44]):
+        last = max(i for i in range(len(keys)) if keys[i] == k)
+        assert T.table_get(got, k) == vals[last]
+
+
+def test_tail_one_key_under_two_khash(codec):
+    """AddIkey lets the caller pick khash: one user key added under two khash
+    values, each group conflicting with other keys.  conflictKeys is one map per
+    table, so the key is written once, with the handle of whichever group
+    assigned it last -- including the case where that assignment is the first
+    key's re-assignment at the add that makes its group conflict."""
+    rng = random.Random(42)
+    A, B = 0x11110000, 0x22220000
+    cases = [
+        # (key, khash): "dup" first in group A (assigned again when A conflicts), later in group B
+        [(b"dup", A), (b"x1", B), (b"dup", B), (b"a2", A)],
+        # dup last assigned in A by a plain re-add after both groups conflict
+        [(b"dup", B), (b"y1", B), (b"dup", A), (b"y2", A), (b"dup", A)],
+        # dup never re-added: B's conflict-making add assigns it after A's
+        [(b"dup", A), (b"z1", A), (b"dup", B), (b"z2", B)],
+    ]
+    for spec in cases:
+        spec = spec + [(b"fill_%d" % i, O.fnv32(b"fill_%d" % i)) for i in range(20)]
+        keys = [k for k, _ in spec]
+        khash = [h for _, h in spec]
+        trs = [((i + 1) << 8) | 1 for i in range(len(spec))]
+        vals = [rb(rng, rng.choice([3, 60])) for _ in spec]
+        got, stats = _ikey_table(codec, keys, trs, vals, khash)
+        exp, w = _oracle_ikey_table(keys, trs, vals, khash)
+        assert int(stats[0, 1]) == len(w.conflict_keys)
+        assert got == exp, spec[:5]
