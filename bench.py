@@ -587,7 +587,7 @@ def run_c3(a, world, rank, local, dev, codec):
     alg = n * (16 + 40 + 1024) + disk
     out["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "traffic": None, "scope": "whole step (k_decode_stream<1> + scan + k_snappy_rt)",
+                       "traffic": None, "scope": "whole step (k_snappy_front + size scan + k_snappy_mat + k_snappy_rt)",
                        "step_event_ms": round(kms, 4)}
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O

@@ -59,6 +59,39 @@ __device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// Wave-wide inclusive scans through DPP (row_shr 1/2/4/8, then row_bcast 15 /
+// 31): no lane-address registers, unlike __shfl_up / ds_bpermute.
+#define BHG_DPP(x, ctrl, rmask) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), ctrl, rmask, 0xf, false))
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += BHG_DPP(x, 0x111, 0xf);
+    x += BHG_DPP(x, 0x112, 0xf);
+    x += BHG_DPP(x, 0x114, 0xf);
+    x += BHG_DPP(x, 0x118, 0xf);
+    x += BHG_DPP(x, 0x142, 0xa);
+    x += BHG_DPP(x, 0x143, 0xc);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {  // values >= 0: 0 is the identity
+    uint32_t y;
+    y = BHG_DPP(x, 0x111, 0xf); x = y > x ? y : x;
+    y = BHG_DPP(x, 0x112, 0xf); x = y > x ? y : x;
+    y = BHG_DPP(x, 0x114, 0xf); x = y > x ? y : x;
+    y = BHG_DPP(x, 0x118, 0xf); x = y > x ? y : x;
+    y = BHG_DPP(x, 0x142, 0xa); x = y > x ? y : x;
+    y = BHG_DPP(x, 0x143, 0xc); x = y > x ? y : x;
+    return x;
+}
+#undef BHG_DPP
+
+// Lanes of a wave hand LDS bytes to each other (one lane writes, another
+// reads): LDS runs a wave's accesses in program order, but the compiler sees
+// one thread and could move a read above another lane's write, so each
+// hand-over is a wavefront-scope fence (LDS types that cross it are may_alias).
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t crc_table_entry(uint32_t i) {
     uint32_t c = i;
 #pragma unroll

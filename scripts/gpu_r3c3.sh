@@ -1,0 +1,19 @@
+#!/bin/bash
+# C3 snappy decode iteration: GPU tests touching the decode, the C3 bench line and
+# its rocprofv3 kernel stats
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${1:-r3c3}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_gpu_c5.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1; rc=$?
+echo "pytest rc=$rc" >> $O/pytest_gpu.txt
+tail -3 $O/pytest_gpu.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --config c3 > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/trace" -o run --output-format csv \
+  -- python3 bench.py --config c3 --no-cpu --warmup 10 > $O/bench_c3_prof.json 2> $O/bench_c3_prof.err || exit 1
+python -c "
+import json; d=json.load(open('$O/bench_c3.json')); r=d.get('roofline',{})
+print('c3', d['value'], d['ms_per_step'], r.get('frac'), r.get('step_event_ms'), d.get('parity_vs_restatement'), d['status_ok_blocks'])"
+find $O/trace -name '*kernel_stats.csv' -exec head -12 {} \;

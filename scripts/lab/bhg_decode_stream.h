@@ -1,5 +1,5 @@
-// bhg_decode_stream.h -- the NoCompressor batch decode for gfx950 (and the
-// header / CRC pass of the snappy decode): readRecordHeader + readRecord +
+// bhg_decode_stream.h (lab only; no longer in the product) -- a NoCompressor batch decode for gfx950 (and
+// round 2's header / CRC pass of the snappy decode, replaced by k_snappy_front): readRecordHeader + readRecord +
 // readKV + FNV-1 + masked CRC-32C per block (bithash/block2.go:31-66,
 // compress.go:57-59, internal/hash/fnv.go:19-23, internal/crc/crc.go:19-33).
 //
@@ -32,8 +32,8 @@
 // LDS: Crc4Perm (slice-by-4 replicated 32x, 128 KiB, conflict free) + the
 // fold table + six scan tables + E = 156.5 KiB -> one workgroup per CU.
 #pragma once
-#include "bhg_crc_tables.h"
-#include "bhg_device.h"
+#include "../../bitalosdb_amd/csrc/bhg_crc_tables.h"
+#include "../../bitalosdb_amd/csrc/bhg_device.h"
 
 namespace bhg {
 
@@ -72,38 +72,8 @@ __device__ __forceinline__ uint32_t ld32_clamp(uint64_t a, uint64_t lo4, uint64_
     return gld<uint32_t>(a < lo4 ? lo4 : (a > hi4 ? hi4 : a));
 }
 
-// Wave-wide inclusive scans through DPP (row_shr 1/2/4/8, then row_bcast 15 /
-// 31): no lane-address registers, unlike __shfl_up / ds_bpermute.
-#define BHG_DPP(x, ctrl, rmask) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x), ctrl, rmask, 0xf, false))
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
-    x += BHG_DPP(x, 0x111, 0xf);
-    x += BHG_DPP(x, 0x112, 0xf);
-    x += BHG_DPP(x, 0x114, 0xf);
-    x += BHG_DPP(x, 0x118, 0xf);
-    x += BHG_DPP(x, 0x142, 0xa);
-    x += BHG_DPP(x, 0x143, 0xc);
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {  // values >= 0: 0 is the identity
-    uint32_t y;
-    y = BHG_DPP(x, 0x111, 0xf); x = y > x ? y : x;
-    y = BHG_DPP(x, 0x112, 0xf); x = y > x ? y : x;
-    y = BHG_DPP(x, 0x114, 0xf); x = y > x ? y : x;
-    y = BHG_DPP(x, 0x118, 0xf); x = y > x ? y : x;
-    y = BHG_DPP(x, 0x142, 0xa); x = y > x ? y : x;
-    y = BHG_DPP(x, 0x143, 0xc); x = y > x ? y : x;
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_or(uint32_t x) {
-    x |= BHG_DPP(x, 0x111, 0xf);
-    x |= BHG_DPP(x, 0x112, 0xf);
-    x |= BHG_DPP(x, 0x114, 0xf);
-    x |= BHG_DPP(x, 0x118, 0xf);
-    x |= BHG_DPP(x, 0x142, 0xa);
-    x |= BHG_DPP(x, 0x143, 0xc);
-    return x;
-}
-#undef BHG_DPP
+using bhg::wave_incl_add;
+using bhg::wave_incl_max;
 
 }  // namespace stream_detail
 

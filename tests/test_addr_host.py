@@ -25,7 +25,7 @@ def helpers(tmp_path_factory):
         pytest.skip("no clang++")
     s = open(HDR).read()
     i0 = s.index("__device__ __forceinline__ uint64_t readlane_u64(")
-    i1 = s.index("__device__ __forceinline__ uint32_t crc_table_entry(")
+    i1 = s.index("// Wave-wide inclusive scans through DPP")
     body = s[i0:i1].replace("__device__ __forceinline__ ", 'extern "C" ')
     # every lane holds the same value, so lane l's register is the argument itself; the
     # stand-ins return it as `int`, as the gfx950 builtins do
