@@ -271,6 +271,41 @@ __device__ __forceinline__ MatInfo mat_info(uint32_t i, uint32_t n, const bhg_de
 
 }  // namespace
 
+// Op replay with dword-aligned LDS accesses only: a 16-B (or 8-B) LDS access
+// off its natural alignment is replayed at 64 cycles per instruction on gfx950,
+// and op sources / destinations sit at any byte.  An op reads the 5 dwords
+// around its source and assembles the 16 bytes with v_perm; it writes 5 dwords
+// from its destination's dword, the first merged with the lane's copy of that
+// dword's final bytes (pend) -- so nothing is read back.  Writes reach 20 B past
+// the cursor (k_snappy_front's in-place margin).
+typedef uint32_t u32_lds __attribute__((may_alias));
+
+template <int BPW, int SLOT>
+__device__ __forceinline__ void mat_replay_op(uint8_t *lds, uint32_t op, bool act, uint32_t slot0, uint32_t trash,
+                                              uint32_t &d, uint32_t &pend) {
+    u32_lds *L = reinterpret_cast<u32_lds *>(lds);
+    const uint32_t src = act ? slot0 + (op & 0x7ffu) : slot0;
+    const uint32_t len = (op >> 11) + 1u;
+    const uint32_t as = src >> 2, sr = src & 3u;
+    const uint32_t r0 = L[as], r1 = L[as + 1], r2 = L[as + 2], r3 = L[as + 3], r4 = L[as + 4];
+    const uint32_t selr = 0x03020100u + sr * 0x01010101u;
+    const uint32_t b0 = __builtin_amdgcn_perm(r1, r0, selr), b1 = __builtin_amdgcn_perm(r2, r1, selr);
+    const uint32_t b2 = __builtin_amdgcn_perm(r3, r2, selr), b3 = __builtin_amdgcn_perm(r4, r3, selr);
+    const uint32_t sh = d & 3u;                                    // slot0 is 16-B aligned
+    const uint32_t selw = 0x07060504u - sh * 0x01010101u;          // bytes [4 - sh, 8 - sh) of (hi:lo)
+    const uint32_t m = (1u << (8u * sh)) - 1u;                     // the sh final bytes of pend
+    const uint32_t sel0 = (0x03020100u & m) | (selw & ~m);
+    const uint32_t q0 = __builtin_amdgcn_perm(b0, pend, sel0), q1 = __builtin_amdgcn_perm(b1, b0, selw);
+    const uint32_t q2 = __builtin_amdgcn_perm(b2, b1, selw), q3 = __builtin_amdgcn_perm(b3, b2, selw);
+    const uint32_t q4 = __builtin_amdgcn_perm(b3, b3, selw);
+    const uint32_t D = (act ? slot0 + d : trash) >> 2;
+    L[D] = q0; L[D + 1] = q1; L[D + 2] = q2; L[D + 3] = q3; L[D + 4] = q4;
+    const uint32_t jn = (sh + len) >> 2;                           // the dword holding the new cursor
+    const uint32_t pn = jn == 0 ? q0 : jn == 1 ? q1 : jn == 2 ? q2 : jn == 3 ? q3 : q4;
+    pend = act ? pn : pend;
+    d += act ? len : 0u;
+}
+
 template <int BPW, int SLOT>
 __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
@@ -279,6 +314,7 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
                                                    const uint32_t *__restrict__ meta,
                                                    const uint16_t *__restrict__ ops) {
     static_assert(SLOT % 16 == 0 && BPW <= 64, "16-B aligned slots, a lane per block");
+    constexpr uint32_t kChunks = kSnapOpCap / 8, kRegChunks = 12;  // 16-B op chunks; the first 96 ops ride in VGPRs
     __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
@@ -290,7 +326,12 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
         const uint32_t i = grp * BPW + lane;
         return mat_info(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, meta, base, out_cap);
     };
+    auto op_chunks = [&](uint32_t grp) -> const u32x4 * {
+        const uint32_t i = grp * BPW + (lane < BPW ? lane : 0u);
+        return reinterpret_cast<const u32x4 *>(ops + (uint64_t)(i < n ? i : n - 1) * kSnapOpCap);
+    };
     u32x4 v[BPW];
+    u32x4 opc[kRegChunks], opn[kRegChunks];
     // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
     // past the stream load src + 0; the dump drops them) and clamped to end
     // src (a chunk that would cross the end is loaded from end - 16 and
@@ -309,11 +350,18 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
             v[b] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
         }
     };
+    auto load_ops = [&](u32x4 (&dst)[kRegChunks], uint32_t grp) {
+        const u32x4 *oc = op_chunks(grp < ngroups ? grp : g);
+#pragma unroll
+        for (uint32_t c = 0; c < kRegChunks; c++) dst[c] = oc[c];
+    };
     MatInfo cur = info(g);
+    load_ops(opc, g);
     prefetch(cur);
     MatInfo nxt = info(g + G);
     for (; g < ngroups; g += G) {
-        // 1. this group's streams -> slots
+        // 1. this group's streams -> slots (the wait here also covers this group's op chunks,
+        //    loaded before the streams)
 #pragma unroll
         for (int b = 0; b < BPW; b++) {
             uint32_t clb;
@@ -330,39 +378,31 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
                 *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + slot_stream_pos(SLOT, clb) + 16 * lane) = c;
         }
         lds_wave_sync();
-        // 2. descriptors of the group after next, then the next group's streams in flight
+        // 2. descriptors of the group after next; the next group's op chunks, then its streams, in flight
         const MatInfo nn = info(g + 2 * G);
+        load_ops(opn, g + G);
         prefetch(nxt);
-        // 3. replay the ops: 8 per 16-B chunk, two chunks in flight
+        // 3. replay the ops (8 per 16-B chunk): the first kRegChunks chunks from VGPRs, the rest loaded here
         const uint32_t nops = cur.mode == SM_LDS ? cur.nops : 0u;
         const uint32_t nch = (nops + 7) >> 3;
         const uint32_t maxc = __builtin_amdgcn_readlane(wave_incl_max(nch), 63);
         if (lane < BPW && maxc) {
-            const uint32_t bi = g * BPW + lane;
-            const u32x4 *oc = reinterpret_cast<const u32x4 *>(ops + (uint64_t)(bi < n ? bi : n - 1) * kSnapOpCap);
-            constexpr uint32_t kChunks = kSnapOpCap / 8;
-            const uint32_t slot0 = lane * SLOT, trash = slot0 + SLOT - 16;
-            uint32_t d = 0;
+            const uint32_t slot0 = lane * SLOT, trash = slot0 + SLOT - 32;
+            uint32_t d = 0, pend = 0;
             auto replay8 = [&](const u32x4 &w, uint32_t c) {
 #pragma unroll
                 for (uint32_t j = 0; j < 8; j++) {
                     const uint32_t word = j < 2 ? w.x : j < 4 ? w.y : j < 6 ? w.z : w.w;
-                    const uint32_t op = (word >> (16 * (j & 1))) & 0xffffu;
-                    const bool act = 8 * c + j < nops;
-                    const uint32_t sa = act ? slot0 + (op & 0x7ffu) : slot0;
-                    const uint32_t da = act ? slot0 + d : trash;
-                    *reinterpret_cast<u32x4_lds_u *>(lds + da) = *reinterpret_cast<const u32x4_lds_u *>(lds + sa);
-                    d += act ? (op >> 11) + 1u : 0u;
+                    mat_replay_op<BPW, SLOT>(lds, (word >> (16 * (j & 1))) & 0xffffu, 8 * c + j < nops, slot0, trash,
+                                             d, pend);
                 }
             };
-            u32x4 oa = oc[0], ob = oc[1 < kChunks ? 1 : 0];
-            for (uint32_t c = 0; c < maxc; c += 2) {
-                replay8(oa, c);
-                oa = oc[c + 2 < kChunks ? c + 2 : 0];
-                if (c + 1 < maxc) {
-                    replay8(ob, c + 1);
-                    ob = oc[c + 3 < kChunks ? c + 3 : 0];
-                }
+#pragma unroll
+            for (uint32_t c = 0; c < kRegChunks; c++)
+                if (c < maxc) replay8(opc[c], c);
+            if (maxc > kRegChunks) {
+                const u32x4 *oc = op_chunks(g);
+                for (uint32_t c = kRegChunks; c < maxc && c < kChunks; c++) replay8(oc[c], c);
             }
         }
         // 4. decoded blocks -> out_vals
@@ -390,6 +430,8 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
         }
         cur = nxt;
         nxt = nn;
+#pragma unroll
+        for (uint32_t c = 0; c < kRegChunks; c++) opc[c] = opn[c];
     }
 }
 

@@ -32,13 +32,15 @@ using namespace bhg;
 // 0 ok (out holds dlen bytes), 1 corrupt, 2 hand over (spill), 3 hand over (op cap)
 extern "C" int walk_replay(const uint8_t *stream, uint32_t clen, uint32_t hdr, uint32_t dlen, uint32_t arena_off,
                            uint8_t *out, uint32_t *nops_out) {
-    std::vector<uint8_t> arena(arena_off + clen + 64 + 16, 0xA5);
+    std::vector<uint8_t> arena_v(arena_off + clen + 64 + 32, 0xA5);
+    uint8_t *arena_base = arena_v.data() + (16 - ((uintptr_t)arena_v.data() & 15));
+    struct { uint8_t *p; uint8_t *data() { return p; } } arena{arena_base};
     memcpy(arena.data() + arena_off, stream, clen);
     std::vector<uint32_t> ops(kSnapOpCap);
     SnapParse S;
     S.s = arena_off + hdr; S.se = arena_off + clen; S.lit0 = slot_stream_pos(kSnapSlot, clen) - arena_off;
     S.d = 0; S.dlen = dlen; S.nops = 0; S.res = 0;
-    S.t8 = *reinterpret_cast<const snap_u64_u *>(arena.data() + S.s);
+    S.t8 = snap_ld8(arena.data(), S.s);
     if (S.s < S.se)
         while (snap_parse_step(arena.data(), S, [&](uint32_t q, uint32_t op) { if (q < kSnapOpCap) ops[q] = op; })) {}
     const uint32_t r = S.res ? S.res : (S.d == S.dlen ? 0u : 1u);
