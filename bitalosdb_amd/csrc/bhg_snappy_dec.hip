@@ -43,6 +43,10 @@
 #include "bhg_internal.h"
 #include "bhg_snappy_parse.h"
 
+#ifndef BHG_MAT_BPW
+#define BHG_MAT_BPW 64  // blocks per wave in k_snappy_mat (2 waves per CU at 64)
+#endif
+
 namespace bhg {
 
 namespace {
@@ -202,40 +206,38 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
-// k_snappy_mat: the value bytes of the blocks k_snappy_front parsed, in LDS.
+// k_snappy_mat: the value bytes of the blocks k_snappy_front parsed.
 //
-// A workgroup is one wave and owns kSnapBPW slots of kSnapSlot bytes, lane b
-// = block b of a group of kSnapBPW consecutive blocks.  A block decodes IN
-// PLACE in its slot: the compressed stream staged at the slot end (P =
-// slot_stream_pos(clen)), the output growing from the slot start.  The tag
-// walk is already done (bhg_snappy_parse.h): the lane replays the block's ops,
-// each one 16-B LDS read + one 16-B LDS write, read from the op scratch 8 at a
-// time (two 16-B chunks in flight).  Per group:
-//   1. the group's streams (prefetched into VGPRs, one 16-B chunk per lane per
-//      block) are written into the slots;
-//   2. the NEXT group's streams are requested (loads in flight during 3-5),
-//      and the descriptors of the group after it;
-//   3. lane b replays block b's ops (status TOO_LARGE / a corrupt stream: no ops);
-//   4. the wave stores each decoded block with contiguous 16-B stores;
-//   5. the descriptors are finalised.
-// 8 waves per CU (two per SIMD) x 18 slots of 1,088 B fill the 160 KiB of LDS.
-// Blocks the front pass could not take (oversize, in-place spill, op cap) were
-// listed for k_snappy_rt, launched after this kernel.
+// A workgroup is one wave; lane b owns block b of a group of BPW consecutive
+// blocks and an LDS slot that holds only its output (kMatSlotDw dwords: an odd
+// stride, so lanes at the same cursor hit different banks).  The tag walk is
+// already done (bhg_snappy_parse.h): the lane replays the block's ops --
+//   literal op: its 16 source bytes come from the stream in global memory,
+//     loaded one chunk of 8 ops ahead;
+//   copy op: 5 dword LDS reads around the source, v_perm'ed into 16 bytes;
+// then 5 dword LDS writes from the cursor's dword, the first merged with the
+// lane's copy of that dword's final bytes (pend), so nothing is read back.
+// Only dword LDS accesses: a misaligned 8- or 16-byte access is replayed at 64
+// cycles per instruction on gfx950, and op sources / cursors sit at any byte.
+// The ops of a group (up to kRegChunks x 8 in VGPRs) are loaded during the
+// previous group.  Per group: replay; each block's output -> out_vals by the
+// whole wave (dword LDS reads, 16-B global stores); descriptors finalised.
+// Blocks the front pass could not take (oversize, op cap) were listed for
+// k_snappy_rt, launched after this kernel.
 // ---------------------------------------------------------------------------
-typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));
-
 namespace {
 
+constexpr uint32_t kMatSlotDw = 261;  // 1,044 B per block: 1,024 + the 20-B write overshoot; odd in dwords
+typedef uint32_t u32_lds __attribute__((may_alias));
+
 // mode of a block in k_snappy_mat
-enum : uint32_t { SM_SKIP = 0, SM_LDS = 1, SM_FINAL = 2 };
+enum : uint32_t { SM_SKIP = 0, SM_OPS = 1, SM_FINAL = 2 };
 
 struct MatInfo {
     uint64_t cp, o0;  // stream (absolute, varint header included), output offset in out_vals
     uint32_t clen, dlen, status, mode, nops;
 };
 
-// All loads first and unconditional (index clamped to n - 1), so the caller can
-// issue them ahead of the stream prefetch and wait for them alone.
 __device__ __forceinline__ MatInfo mat_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
                                             const uint64_t *val_off, const uint32_t *meta, uint64_t base,
                                             uint64_t out_cap) {
@@ -254,7 +256,7 @@ __device__ __forceinline__ MatInfo mat_info(uint32_t i, uint32_t n, const bhg_de
     r.nops = m >> 8;
     r.status = st;
     r.mode = SM_SKIP;
-    if (i < n && (m & 3u) == SNAP_LDS && (st == BHG_ST_OK || st == BHG_ST_CRC_MISMATCH)) {
+    if (i < n && (m & 3u) == SNAP_OPS && (st == BHG_ST_OK || st == BHG_ST_CRC_MISMATCH)) {
         // snappy.Decode's order: the output capacity first, then the stream (decode_other.go)
         if (o1 > out_cap || o1 - o0 < dlen) {
             r.status = BHG_ST_SNAPPY_TOO_LARGE;
@@ -263,59 +265,33 @@ __device__ __forceinline__ MatInfo mat_info(uint32_t i, uint32_t n, const bhg_de
             r.status = BHG_ST_SNAPPY_CORRUPT;
             r.mode = SM_FINAL;
         } else {
-            r.mode = SM_LDS;
+            r.mode = SM_OPS;
         }
     }
     return r;
 }
 
-}  // namespace
-
-// Op replay with dword-aligned LDS accesses only: a 16-B (or 8-B) LDS access
-// off its natural alignment is replayed at 64 cycles per instruction on gfx950,
-// and op sources / destinations sit at any byte.  An op reads the 5 dwords
-// around its source and assembles the 16 bytes with v_perm; it writes 5 dwords
-// from its destination's dword, the first merged with the lane's copy of that
-// dword's final bytes (pend) -- so nothing is read back.  Writes reach 20 B past
-// the cursor (k_snappy_front's in-place margin).
-typedef uint32_t u32_lds __attribute__((may_alias));
-
-template <int BPW, int SLOT>
-__device__ __forceinline__ void mat_replay_op(uint8_t *lds, uint32_t op, bool act, uint32_t slot0, uint32_t trash,
-                                              uint32_t &d, uint32_t &pend) {
-    u32_lds *L = reinterpret_cast<u32_lds *>(lds);
-    const uint32_t src = act ? slot0 + (op & 0x7ffu) : slot0;
-    const uint32_t len = (op >> 11) + 1u;
-    const uint32_t as = src >> 2, sr = src & 3u;
-    const uint32_t r0 = L[as], r1 = L[as + 1], r2 = L[as + 2], r3 = L[as + 3], r4 = L[as + 4];
-    const uint32_t selr = 0x03020100u + sr * 0x01010101u;
-    const uint32_t b0 = __builtin_amdgcn_perm(r1, r0, selr), b1 = __builtin_amdgcn_perm(r2, r1, selr);
-    const uint32_t b2 = __builtin_amdgcn_perm(r3, r2, selr), b3 = __builtin_amdgcn_perm(r4, r3, selr);
-    const uint32_t sh = d & 3u;                                    // slot0 is 16-B aligned
-    const uint32_t selw = 0x07060504u - sh * 0x01010101u;          // bytes [4 - sh, 8 - sh) of (hi:lo)
-    const uint32_t m = (1u << (8u * sh)) - 1u;                     // the sh final bytes of pend
-    const uint32_t sel0 = (0x03020100u & m) | (selw & ~m);
-    const uint32_t q0 = __builtin_amdgcn_perm(b0, pend, sel0), q1 = __builtin_amdgcn_perm(b1, b0, selw);
-    const uint32_t q2 = __builtin_amdgcn_perm(b2, b1, selw), q3 = __builtin_amdgcn_perm(b3, b2, selw);
-    const uint32_t q4 = __builtin_amdgcn_perm(b3, b3, selw);
-    const uint32_t D = (act ? slot0 + d : trash) >> 2;
-    L[D] = q0; L[D + 1] = q1; L[D + 2] = q2; L[D + 3] = q3; L[D + 4] = q4;
-    const uint32_t jn = (sh + len) >> 2;                           // the dword holding the new cursor
-    const uint32_t pn = jn == 0 ? q0 : jn == 1 ? q1 : jn == 2 ? q2 : jn == 3 ? q3 : q4;
-    pend = act ? pn : pend;
-    d += act ? len : 0u;
+// 16 loaded stream bytes that were fetched from end - 16 instead of a (a + 16 > end), shifted into place
+__device__ __forceinline__ u32x4 shift_down(u32x4 c, uint32_t sh) {
+    unsigned __int128 x = (unsigned __int128)c.x | ((unsigned __int128)c.y << 32) | ((unsigned __int128)c.z << 64) |
+                          ((unsigned __int128)c.w << 96);
+    x >>= 8 * sh;
+    return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
 }
 
-template <int BPW, int SLOT>
+}  // namespace
+
+template <int BPW>
 __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off,
                                                    const uint32_t *__restrict__ meta,
                                                    const uint16_t *__restrict__ ops) {
-    static_assert(SLOT % 16 == 0 && BPW <= 64, "16-B aligned slots, a lane per block");
+    static_assert(BPW <= 64, "a lane per block");
     constexpr uint32_t kChunks = kSnapOpCap / 8, kRegChunks = 12;  // 16-B op chunks; the first 96 ops ride in VGPRs
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
+    __shared__ uint32_t lds[BPW * kMatSlotDw + 8];
+    u32_lds *const L = reinterpret_cast<u32_lds *>(lds);
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
     const uint32_t ngroups = (n + BPW - 1) / BPW;
@@ -327,100 +303,115 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
         return mat_info(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, meta, base, out_cap);
     };
     auto op_chunks = [&](uint32_t grp) -> const u32x4 * {
-        const uint32_t i = grp * BPW + (lane < BPW ? lane : 0u);
+        const uint32_t i = (grp < ngroups ? grp : g) * BPW + (lane < BPW ? lane : 0u);
         return reinterpret_cast<const u32x4 *>(ops + (uint64_t)(i < n ? i : n - 1) * kSnapOpCap);
     };
-    u32x4 v[BPW];
     u32x4 opc[kRegChunks], opn[kRegChunks];
-    // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
-    // past the stream load src + 0; the dump drops them) and clamped to end
-    // src (a chunk that would cross the end is loaded from end - 16 and
-    // shifted into place at the dump), so no branch and no wait is tied to the
-    // loads until the next dump.  (The launcher sends src_len < 64 elsewhere.)
-    auto chunk_addr = [&](const MatInfo &I, int b, uint32_t &clb) -> uint64_t {
-        clb = __builtin_amdgcn_readlane(I.mode == SM_LDS ? I.clen : 0u, b);
-        const uint64_t cpb = readlane_u64(I.cp, b);
-        return 16 * lane < clb ? cpb + 16 * lane : base;
-    };
-    auto prefetch = [&](const MatInfo &I) {
-#pragma unroll
-        for (int b = 0; b < BPW; b++) {
-            uint32_t clb;
-            const uint64_t a = chunk_addr(I, b, clb);
-            v[b] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
-        }
-    };
     auto load_ops = [&](u32x4 (&dst)[kRegChunks], uint32_t grp) {
-        const u32x4 *oc = op_chunks(grp < ngroups ? grp : g);
+        const u32x4 *oc = op_chunks(grp);
 #pragma unroll
         for (uint32_t c = 0; c < kRegChunks; c++) dst[c] = oc[c];
     };
     MatInfo cur = info(g);
     load_ops(opc, g);
-    prefetch(cur);
     MatInfo nxt = info(g + G);
     for (; g < ngroups; g += G) {
-        // 1. this group's streams -> slots (the wait here also covers this group's op chunks,
-        //    loaded before the streams)
-#pragma unroll
-        for (int b = 0; b < BPW; b++) {
-            uint32_t clb;
-            const uint64_t a = chunk_addr(cur, b, clb);
-            u32x4 c = v[b];
-            if (a + 16 > end) {  // the chunk was loaded from end - 16: its bytes start at a - (end - 16)
-                const uint32_t sh = (uint32_t)(a - (end - 16));
-                unsigned __int128 x = (unsigned __int128)c.x | ((unsigned __int128)c.y << 32) |
-                                      ((unsigned __int128)c.z << 64) | ((unsigned __int128)c.w << 96);
-                x >>= 8 * sh;
-                c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
-            }
-            if (16 * lane < clb)
-                *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + slot_stream_pos(SLOT, clb) + 16 * lane) = c;
-        }
-        lds_wave_sync();
-        // 2. descriptors of the group after next; the next group's op chunks, then its streams, in flight
+        // the next group's op chunks, and the descriptors of the group after it, in flight
         const MatInfo nn = info(g + 2 * G);
         load_ops(opn, g + G);
-        prefetch(nxt);
-        // 3. replay the ops (8 per 16-B chunk): the first kRegChunks chunks from VGPRs, the rest loaded here
-        const uint32_t nops = cur.mode == SM_LDS ? cur.nops : 0u;
+        const uint32_t nops = cur.mode == SM_OPS ? cur.nops : 0u;
         const uint32_t nch = (nops + 7) >> 3;
         const uint32_t maxc = __builtin_amdgcn_readlane(wave_incl_max(nch), 63);
         if (lane < BPW && maxc) {
-            const uint32_t slot0 = lane * SLOT, trash = slot0 + SLOT - 32;
+            const uint32_t slot0 = lane * kMatSlotDw;  // dwords
+            const uint32_t trash = slot0 + kMatSlotDw - 5;
             uint32_t d = 0, pend = 0;
-            auto replay8 = [&](const u32x4 &w, uint32_t c) {
+            // literal sources of one chunk of 8 ops (copy ops load the stream's first bytes, unused)
+            auto lit_loads = [&](const u32x4 &w, u32x4 (&lb)[8]) {
 #pragma unroll
                 for (uint32_t j = 0; j < 8; j++) {
                     const uint32_t word = j < 2 ? w.x : j < 4 ? w.y : j < 6 ? w.z : w.w;
-                    mat_replay_op<BPW, SLOT>(lds, (word >> (16 * (j & 1))) & 0xffffu, 8 * c + j < nops, slot0, trash,
-                                             d, pend);
+                    const uint32_t op = (word >> (16 * (j & 1))) & 0xffffu;
+                    const uint32_t so = op >> 15 ? op & 0x7ffu : 0u;
+                    const uint64_t a = cur.cp + so < end ? cur.cp + so : base;
+                    lb[j] = gld<u32x4u>(a + 16 <= end ? a : end - 16);  // unconditional: no wait tied to a branch
                 }
             };
+            auto replay8 = [&](const u32x4 &w, const u32x4 (&lb)[8], uint32_t c) {
 #pragma unroll
-            for (uint32_t c = 0; c < kRegChunks; c++)
-                if (c < maxc) replay8(opc[c], c);
-            if (maxc > kRegChunks) {
-                const u32x4 *oc = op_chunks(g);
-                for (uint32_t c = kRegChunks; c < maxc && c < kChunks; c++) replay8(oc[c], c);
+                for (uint32_t j = 0; j < 8; j++) {
+                    const uint32_t word = j < 2 ? w.x : j < 4 ? w.y : j < 6 ? w.z : w.w;
+                    const uint32_t op = (word >> (16 * (j & 1))) & 0xffffu;
+                    const bool act = 8 * c + j < nops;
+                    const bool lit = (op >> 15) != 0u;
+                    const uint32_t len = ((op >> 11) & 15u) + 1u;
+                    u32x4 lv = lb[j];
+                    if (__ballot(lit && cur.cp + (op & 0x7ffu) + 16 > end) != 0) {  // only at the very end of src
+                        const uint64_t a = cur.cp + (op & 0x7ffu);
+                        if (lit && a + 16 > end) lv = shift_down(lv, (uint32_t)(a - (end - 16)));
+                    }
+                    uint32_t b0 = lv.x, b1 = lv.y, b2 = lv.z, b3 = lv.w;
+                    if (!lit) {  // copy: the 16 output bytes at src, from the 5 dwords around them
+                        const uint32_t sa = slot0 + ((op & 0x7ffu) >> 2), sr = op & 3u;
+                        const uint32_t r0 = L[sa], r1 = L[sa + 1], r2 = L[sa + 2], r3 = L[sa + 3], r4 = L[sa + 4];
+                        const uint32_t selr = 0x03020100u + sr * 0x01010101u;
+                        b0 = __builtin_amdgcn_perm(r1, r0, selr);
+                        b1 = __builtin_amdgcn_perm(r2, r1, selr);
+                        b2 = __builtin_amdgcn_perm(r3, r2, selr);
+                        b3 = __builtin_amdgcn_perm(r4, r3, selr);
+                    }
+                    const uint32_t sh = d & 3u;
+                    const uint32_t selw = 0x07060504u - sh * 0x01010101u;  // bytes [4 - sh, 8 - sh) of (hi:lo)
+                    const uint32_t m = (1u << (8u * sh)) - 1u;            // the sh final bytes of pend
+                    const uint32_t sel0 = (0x03020100u & m) | (selw & ~m);
+                    const uint32_t q0 = __builtin_amdgcn_perm(b0, pend, sel0), q1 = __builtin_amdgcn_perm(b1, b0, selw);
+                    const uint32_t q2 = __builtin_amdgcn_perm(b2, b1, selw), q3 = __builtin_amdgcn_perm(b3, b2, selw);
+                    const uint32_t q4 = __builtin_amdgcn_perm(b3, b3, selw);
+                    const uint32_t D = act ? slot0 + (d >> 2) : trash;
+                    L[D] = q0; L[D + 1] = q1; L[D + 2] = q2; L[D + 3] = q3; L[D + 4] = q4;
+                    const uint32_t jn = (sh + len) >> 2;  // the dword holding the new cursor
+                    const uint32_t pn = jn == 0 ? q0 : jn == 1 ? q1 : jn == 2 ? q2 : jn == 3 ? q3 : q4;
+                    pend = act ? pn : pend;
+                    d += act ? len : 0u;
+                }
+            };
+            u32x4 la[8], lb[8];
+            lit_loads(opc[0], la);
+#pragma unroll
+            for (uint32_t c = 0; c < kRegChunks; c += 2) {
+                if (c < maxc) {
+                    if (c + 1 < kRegChunks) lit_loads(opc[c + 1], lb);
+                    replay8(opc[c], la, c);
+                }
+                if (c + 1 < maxc) {
+                    if (c + 2 < kRegChunks) lit_loads(opc[c + 2], la);
+                    replay8(opc[c + 1], lb, c + 1);
+                }
             }
-        }
-        // 4. decoded blocks -> out_vals
-        lds_wave_sync();
-        {
-            const uint32_t dl = cur.mode == SM_LDS ? cur.dlen : 0u;
-#pragma unroll
-            for (int b = 0; b < BPW; b++) {
-                const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
-                if (16 * lane < dlb) {
-                    const uint64_t ob = (uint64_t)out_vals + readlane_u64(cur.o0, b);
-                    st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + 16 * lane),
-                              ob + dlb);
+            if (maxc > kRegChunks) {  // more than kRegChunks x 8 ops: the rest straight from the op scratch
+                const u32x4 *oc = op_chunks(g);
+                for (uint32_t c = kRegChunks; c < maxc && c < kChunks; c++) {
+                    const u32x4 w = oc[c];
+                    lit_loads(w, la);
+                    replay8(w, la, c);
                 }
             }
         }
         lds_wave_sync();
-        // 5. descriptors
+        // each block's output -> out_vals: the wave stores one block at a time, 16 B per lane
+        {
+            const uint32_t dl = cur.mode == SM_OPS ? cur.dlen : 0u;
+            for (int b = 0; b < BPW; b++) {
+                const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
+                if (dlb == 0) continue;  // uniform
+                if (16 * lane < dlb) {
+                    const uint64_t ob = (uint64_t)out_vals + readlane_u64(cur.o0, b);
+                    const uint32_t a = b * kMatSlotDw + 4 * lane;
+                    st16_clip(ob + 16 * lane, u32x4{L[a], L[a + 1], L[a + 2], L[a + 3]}, ob + dlb);
+                }
+            }
+        }
+        lds_wave_sync();
         if (cur.mode != SM_SKIP) {
             uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
             const bool ok = cur.status == BHG_ST_OK || cur.status == BHG_ST_CRC_MISMATCH;
@@ -438,20 +429,20 @@ __global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ s
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          const uint32_t *meta, const uint16_t *ops, const uint32_t *list) {
-    if (src_len >= 64 && meta && ops && list) {
-        constexpr uint32_t BPW = kSnapBPW, SLOT = kSnapSlot;
-        // resident workgroups per CU (LDS-bound: 8 at 18 x 1,088 B); a grid past that would
-        // start its extra workgroups only when the first ones finish
+    if (src_len >= 16 && meta && ops && list) {
+        constexpr uint32_t BPW = BHG_MAT_BPW;
+        // resident workgroups per CU (LDS-bound); a grid past that would start its extra
+        // workgroups only when the first ones finish
         static const uint32_t per_cu =
-            resident_per_cu((const void *)k_snappy_mat<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
+            resident_per_cu((const void *)k_snappy_mat<BPW>, 64, (160u * 1024u) / (BPW * kMatSlotDw * 4 + 32));
         const uint32_t groups = (n + BPW - 1) / BPW;
         const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
         uint32_t grid = groups < cap ? groups : cap;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_snappy_mat<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+        hipLaunchKernelGGL((k_snappy_mat<BPW>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
                            out_vals, out_cap, val_off, meta, ops);
         if (hipError_t e = hipGetLastError()) return e;
-        // then the blocks the front pass listed (too big for a slot, spill, op cap), lane per block from global memory
+        // then the blocks the front pass listed (oversize, op cap), lane per block from global memory
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
                            out_cap, val_off, list);
         return hipGetLastError();

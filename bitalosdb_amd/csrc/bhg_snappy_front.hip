@@ -6,7 +6,7 @@
 // whole record (internal/crc/crc.go:19-33), snappy's
 // decodedLen (the sizes the output-offset scan needs), and the tag walk of
 // golang/snappy's decode (compress.go:83-85), which turns the block into the
-// 16-byte LDS copy ops k_snappy_mat replays (bhg_snappy_parse.h).
+// 16-byte copy ops k_snappy_mat replays (bhg_snappy_parse.h).
 //
 // A wave takes tiles of 64 consecutive handles, lane = record (the next
 // tile's handles and expected CRCs are loaded while a tile is processed):
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64 * kFrontWaves) void k_snappy_front(
             lds_wave_sync();
             // head words, the walk set-up (decodedLen), then the CRC and the tag walk in one loop
             SnapParse S;
-            S.s = S.se = 0; S.lit0 = 0; S.d = 0; S.dlen = 0; S.nops = 0; S.res = 0; S.t8 = 0;
+            S.s = S.se = S.sb = 0; S.d = 0; S.dlen = 0; S.nops = 0; S.res = 0; S.t8 = 0;
             bool par = false;
             if (go) {
 #pragma unroll
@@ -213,14 +213,14 @@ __global__ __launch_bounds__(64 * kFrontWaves) void k_snappy_front(
                     dsize = dl_ok ? xx : 0;
                     if (dl_ok) {
                         mode = SNAP_GLOBAL;
-                        if (walk && xx <= 1024u && v <= 1024u && v + 24u <= kSnapSlot) {
+                        if (walk && xx <= kSnapMaxOut && v <= kSnapMaxStream) {
                             S.s = vb + hdr;
                             S.se = vb + v;
-                            S.lit0 = slot_stream_pos(kSnapSlot, v) - vb;
+                            S.sb = vb;
                             S.dlen = (uint32_t)xx;
                             S.t8 = snap_ld8(arena, S.s);
                             par = S.s < S.se;
-                            mode = SNAP_LDS;
+                            mode = SNAP_OPS;
                         }
                     }
                 }
@@ -242,13 +242,13 @@ __global__ __launch_bounds__(64 * kFrontWaves) void k_snappy_front(
                     }
                 }
                 if (par)
-                    par = snap_parse_step(arena, S, [&](uint32_t q, uint32_t op) {
-                        if (q < kSnapOpCap) opp[q] = (uint16_t)op;
+                    par = snap_parse_step(arena, S, [&](uint32_t q, uint32_t op, bool on) {
+                        if (on && q < kSnapOpCap) opp[q] = (uint16_t)op;
                     });
             }
-            if (go && mode == SNAP_LDS) {
+            if (go && mode == SNAP_OPS) {
                 const uint32_t r = S.res ? S.res : (S.d == S.dlen ? 0u : 1u);
-                if (r == 2 || (r == 0 && S.nops > kSnapOpCap)) mode = SNAP_GLOBAL;
+                if (r == 0 && S.nops > kSnapOpCap) mode = SNAP_GLOBAL;  // too many ops: k_snappy_rt
                 else if (r == 1) corrupt = 1;
                 nops = S.nops;
             }

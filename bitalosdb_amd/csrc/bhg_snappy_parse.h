@@ -1,33 +1,33 @@
 // bhg_snappy_parse.h -- golang/snappy v0.0.4 block parse (decode_other.go
 // `decode`, called by internal/compress/compress.go:83-85) into 16-byte
-// copy OPS for the LDS materialiser (k_snappy_mat, bhg_snappy_dec.hip).
+// copy OPS for the materialiser (k_snappy_mat, bhg_snappy_dec.hip).
 //
 // The decode is split in two kernels.  k_snappy_front (bhg_snappy_front.hip)
 // stages a tile of records in LDS, CRCs them and walks each block's tag
 // stream, lane per block, 64 blocks per wave, writing for every element the
-// ops that produce it; k_snappy_mat later replays the ops of 18 blocks per
-// wave in their LDS slots, where nothing is left to decode.
+// ops that produce it; k_snappy_mat later replays the ops of 64 blocks per
+// wave, the output in LDS, where nothing is left to decode.
 //
-// The slot (SLOT bytes per block in k_snappy_mat) holds the block in place:
-// the compressed stream staged at P = slot_stream_pos(clen), the output
-// growing from offset 0.  An op is
-//     src | (len - 1) << 11       (src: slot offset < 2048, len 1..16)
-// and means: read the 16 bytes at slot offset src, write them at the output
-// cursor, advance the cursor by len (the replay writes up to 20 bytes).  Only the first len bytes written are
-// final; the rest are overwritten by the next ops in program order (LDS runs a
-// wave's accesses in order).  Per element:
-//   literal of n bytes at stream position q:   ops (P + q + 16 j, <= 16)
-//   copy (offset o, length n), o >= min(n, 16): ops (d - o + 16 j, <= 16)
+// An op is a u16:
+//     src | (len - 1) << 11 | lit << 15      (src < 2048, len 1..16)
+// lit: the len bytes at stream offset src (the value's bytes, varint header
+// included) are output bytes; copy: the len bytes at output offset src are.
+// The replay reads 16 bytes from the source and writes them at the output
+// cursor (5 dwords from the cursor's dword), then advances the cursor by len:
+// only the first len bytes are final, the rest are rewritten by the following
+// ops in program order.  Per element:
+//   literal of n bytes at stream offset q:           ops (q + 16 j, <= 16)
+//   copy (offset o, length n), o >= min(n, 16):      ops (d - o + 16 j, <= 16)
 //   copy with a short period o < min(n, 16): the first op copies o bytes from
 //     d - o, and while the period e < 16 every op copies e bytes from e bytes
 //     back and doubles e (the bytes [d - o, cursor) are periodic, so e bytes
 //     back is always the right phase); then 16 bytes per op from e back.
-// The checks are decode_other.go's, check for check: literal length bytes
-// past the input, literal longer than the remaining input or output, copy
-// offset 0 or beyond the bytes written, copy past dlen, d == dlen at the end.
-// A block whose 16-B writes would reach its own unread stream bytes (in
-// place), or that needs more than kSnapOpCap ops, is handed to the
-// global-memory decoder (k_snappy_rt).
+// The first four ops of an element are emitted straight-line (every C3 element
+// needs at most four); longer elements loop.  The checks are
+// decode_other.go's, check for check: literal length bytes past the input,
+// literal longer than the remaining input or output, copy offset 0 or beyond
+// the bytes written, copy past dlen, d == dlen at the end.  A block that needs
+// kSnapOpCap ops or more is handed to the global-memory decoder (k_snappy_rt).
 // tests/test_snappy_walk_host.py compiles this file for the host and checks
 // parse + op replay against the restated decoder.
 #pragma once
@@ -37,31 +37,28 @@ namespace bhg {
 
 typedef uint64_t snap_u64_a __attribute__((aligned(8), may_alias));
 
-constexpr uint32_t kSnapOpCap = 192;  // ops per block (u16 each) in the op scratch
-constexpr uint32_t kSnapSlot = 1088;  // k_snappy_mat slot bytes per block (the 1 KiB value + stream room)
-constexpr uint32_t kSnapBPW = 18;     // k_snappy_mat blocks per wave (8 waves x 18 slots fill 160 KiB)
+constexpr uint32_t kSnapOpCap = 192;     // u16 op slots per block in the op scratch; the last is a dump slot
+constexpr uint32_t kSnapMaxOut = 1024;   // decoded lengths the op path takes (larger: k_snappy_rt)
+constexpr uint32_t kSnapMaxStream = 2047;  // stream lengths the op path takes (op src is 11 bits)
 
 // how a block's value is decoded (k_snappy_front -> meta)
-enum : uint32_t { SNAP_SKIP = 0, SNAP_LDS = 1, SNAP_GLOBAL = 2 };
-
-// slot offset of a stream of clen bytes (16-B aligned, 8 B of tag over-read room after it)
-__device__ __forceinline__ uint32_t slot_stream_pos(uint32_t slot, uint32_t clen) {
-    return (slot - 8u - ((clen + 15u) & ~15u)) & ~15u;
-}
+enum : uint32_t { SNAP_SKIP = 0, SNAP_OPS = 1, SNAP_GLOBAL = 2 };
 
 // one block's parse state; LDS byte offsets into the staging arena
 struct SnapParse {
     uint32_t s;      // next tag
     uint32_t se;     // end of the stream
-    uint32_t lit0;   // slot offset of arena offset 0 (mod 2^32): slot(x) = lit0 + x
+    uint32_t sb;     // the stream's first byte (stream offset 0)
     uint32_t d;      // output bytes so far
     uint32_t dlen;   // decoded length (from the varint header)
     uint32_t nops;   // ops emitted
-    uint32_t res;    // 0 ok so far, 1 snappy.ErrCorrupt, 2 hand over to the global-memory decoder
+    uint32_t res;    // 0 ok so far, 1 snappy.ErrCorrupt
     uint64_t t8;     // the tag at s and the bytes after it
 };
 
-__device__ __forceinline__ uint32_t snap_op(uint32_t src, uint32_t len) { return src | ((len - 1u) << 11); }
+__device__ __forceinline__ uint32_t snap_op(uint32_t src, uint32_t len, uint32_t lit) {
+    return src | ((len - 1u) << 11) | (lit << 15);
+}
 
 // The 8 bytes at LDS offset p from two 8-aligned 8-byte reads (misaligned
 // 8- and 16-byte LDS accesses are replayed at 64 cycles per instruction on
@@ -73,9 +70,10 @@ __device__ __forceinline__ uint64_t snap_ld8(const uint8_t *lds, uint32_t p) {
     return s ? (x0 >> (8u * s)) | (x1 << (64u - 8u * s)) : x0;
 }
 
-// One element.  emit(k, op) receives op k of the block.  Returns true while
-// more elements follow.  The tag decode is straight-line (selects, no per-type
-// branches); the next tag is read before the ops are emitted.
+// One element.  emit(k, op, on) stores op k of the block when `on` (a slot the
+// element does not use may be stored anywhere harmless).  Returns true while
+// more elements follow.  The tag decode is straight-line (selects, no
+// per-type branches); the next tag is read before the ops are emitted.
 template <class Emit>
 __device__ __forceinline__ bool snap_parse_step(const uint8_t *lds, SnapParse &S, Emit &&emit) {
     const uint64_t t8 = S.t8;
@@ -98,28 +96,31 @@ __device__ __forceinline__ bool snap_parse_step(const uint8_t *lds, SnapParse &S
     const uint32_t bad_lit = (uint32_t)(n > rem - adv), bad_cp = (uint32_t)(off == 0u) | (uint32_t)(off > d);
     const bool bad = ((uint32_t)(adv > rem) | (uint32_t)(n > S.dlen - d) | (uint32_t)(n == 0u) | (mlit & bad_lit) |
                       (~mlit & bad_cp)) != 0u;
-    const uint32_t sn = s + adv + (mlit & n);
-    // in place: the element's writes (5 dwords from the cursor's dword) end below d + n + 20, the
-    // next unread stream byte is at slot(sn)
-    const bool spill = d + n + 20u > S.lit0 + sn;
-    if (bad | spill) {
-        S.res = bad ? 1u : 2u;
+    if (bad) {
+        S.res = 1u;
         return false;
     }
+    const uint32_t sn = s + adv + (mlit & n);
     S.t8 = snap_ld8(lds, sn);  // next tag, in flight while the ops go out
-    const bool lit = mlit != 0u;
-    const uint32_t lsrc = S.lit0 + s + adv;
-    uint32_t e = lit ? 16u : off;
-    // first op (every element has one), then the rest (elements over 16 B, short periods)
-    uint32_t cap = e < 16u ? e : 16u;
-    uint32_t len = n < cap ? n : cap;
-    emit(S.nops, snap_op(lit ? lsrc : d - e, len));
-    uint32_t k = S.nops + 1u, w = len;
-    if (!lit && e < 16u) e <<= 1;
-    while (w < n) {
-        cap = e < 16u ? e : 16u;
-        len = n - w < cap ? n - w : cap;
-        emit(k, snap_op(lit ? lsrc + w : d + w - e, len));
+    const uint32_t lit = mlit & 1u;
+    const uint32_t lsrc = s + adv - S.sb;
+    // ops 0..3 straight-line: e = how far back a copy op reads (a literal's ops step by 16)
+    uint32_t e = lit ? 16u : off, w = 0, k = S.nops;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t cap = e < 16u ? e : 16u;
+        const uint32_t left = n - w;  // 0 once the element is done
+        const uint32_t len = left < cap ? left : cap;
+        const bool on = len != 0u;
+        emit(k, snap_op(lit ? lsrc + w : d + w - e, on ? len : 1u, lit), on);
+        k += on ? 1u : 0u;
+        w += len;
+        if (!lit && e < 16u) e <<= 1;
+    }
+    while (w < n) {  // literals over 64 bytes, short-period copies over four ops
+        const uint32_t cap = e < 16u ? e : 16u;
+        const uint32_t len = n - w < cap ? n - w : cap;
+        emit(k, snap_op(lit ? lsrc + w : d + w - e, len, lit), true);
         k++;
         w += len;
         if (!lit && e < 16u) e <<= 1;
