@@ -30,6 +30,7 @@ struct bhg_ctx {
     void *h_aux = nullptr; size_t h_aux_cap = 0;
     void *h_vals = nullptr; size_t h_vals_cap = 0;
     uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
+    uint32_t *stab = nullptr;  // stream-kernel shift tables (bhg_decode_stream.h build_stream_tab)
     // pipelined host path: kPipe slots, each with its own stream and device ring buffers
     static constexpr int kPipe = 3;
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
@@ -63,6 +64,7 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     L.stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
     L.num_cus = c->num_cus;
     L.ztab = c->ztab;
+    L.stab = c->stab;
     return L;
 }
 
@@ -165,6 +167,12 @@ bhg_ctx *bhg_create(int device, int flags) {
         ok = hipMalloc(reinterpret_cast<void **>(&c->ztab), z.size() * 4) == hipSuccess &&
              hipMemcpy(c->ztab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
+    if (ok) {
+        std::vector<uint32_t> z(bhg::stream_tab_words());
+        bhg::build_stream_tab_default(z.data());
+        ok = hipMalloc(reinterpret_cast<void **>(&c->stab), z.size() * 4) == hipSuccess &&
+             hipMemcpy(c->stab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
     if (!ok) {
         bhg_destroy(c);
         return nullptr;
@@ -184,6 +192,7 @@ void bhg_destroy(bhg_ctx *c) {
     if (c->h_aux) (void)hipFree(c->h_aux);
     if (c->h_vals) (void)hipFree(c->h_vals);
     if (c->ztab) (void)hipFree(c->ztab);
+    if (c->stab) (void)hipFree(c->stab);
     if (c->pool) {
         (void)hipDeviceSynchronize();  // frees enqueued on caller streams have completed
         (void)hipMemPoolDestroy(c->pool);
@@ -269,28 +278,16 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
-    if (codec == BHG_CODEC_NONE) {
-        HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, expected_crc, out_desc));
-        return BHG_OK;
+    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
+    if (codec == BHG_CODEC_SNAPPY) {
+        Scratch sc;
+        const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
+        if (int r = scratch_alloc(c, L.stream, scan_b + (out_vals ? bhg::snappy_list_bytes(n) : 0), sc)) return r;
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
+        if (out_vals)
+            HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off,
+                                          reinterpret_cast<uint32_t *>(sc.base + scan_b)));
     }
-    // SnappyCompressor: front pass (descriptors, decoded sizes into out_val_off, tag walk -> ops) ->
-    // size scan -> value bytes.  A size probe (out_vals null) runs the front pass without the walk.
-    Scratch sc;
-    const size_t scan_b = bhg::scan_scratch_bytes(n);
-    const size_t list_b = out_vals ? bhg::snappy_list_bytes(n) : 0, meta_b = out_vals ? (size_t)n * 4 : 0;
-    const size_t ops_b = out_vals ? bhg::snappy_ops_bytes(n) : 0;
-    if (int r = scratch_alloc(c, L.stream, scan_b + list_b + meta_b + ops_b + 4 * 256, sc)) return r;
-    void *scan_s = sc.take(scan_b);
-    uint32_t *list = out_vals ? reinterpret_cast<uint32_t *>(sc.take(list_b)) : nullptr;
-    uint32_t *meta = out_vals ? reinterpret_cast<uint32_t *>(sc.take(meta_b)) : nullptr;
-    uint16_t *ops = out_vals ? reinterpret_cast<uint16_t *>(sc.take(ops_b)) : nullptr;
-    if (list) HIP_TRY(c, hipMemsetAsync(list, 0, 4, L.stream));
-    HIP_TRY(c, bhg::launch_snappy_front(L, src, src_len, handles, n, expected_crc, out_desc, out_val_off, meta, ops,
-                                        list));
-    HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, scan_s));
-    if (out_vals)
-        HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off, meta,
-                                      ops, list));
     return BHG_OK;
 }
 
@@ -362,7 +359,7 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
         if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc + a, (size_t)cn * 4, hipMemcpyHostToDevice, s));
         bhg::Launch Ls = L;
         Ls.stream = s;
-        HIP_TRY(c, bhg::launch_decode(Ls, base - lo, hi, dh, cn, de, dd));
+        HIP_TRY(c, bhg::launch_decode(Ls, base - lo, hi, dh, cn, BHG_CODEC_NONE, de, dd, nullptr));
         HIP_TRY(c, hipMemcpyAsync(out_desc + a, dd, (size_t)cn * sizeof(bhg_desc), hipMemcpyDeviceToHost, s));
         a = b;
         slot = (slot + 1) % bhg_ctx::kPipe;
@@ -413,7 +410,7 @@ int decode_host_mapped(bhg_ctx *c, const uint8_t *dsrc, uint64_t src_len, const 
         else HIP_TRY(c, hipMemcpyAsync(de, expected_crc, eb, hipMemcpyHostToDevice, s));
     }
     bhg::Launch L = launch_of(c, nullptr);
-    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, de, ddesc ? ddesc : dd));
+    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, BHG_CODEC_NONE, de, ddesc ? ddesc : dd, nullptr));
     if (!ddesc) HIP_TRY(c, hipMemcpyAsync(out_desc, dd, db, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     return BHG_OK;
@@ -452,32 +449,24 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     const size_t eb = expected_crc ? (size_t)n * 4 : 0, ob = codec == BHG_CODEC_SNAPPY ? ((size_t)n + 1) * 8 : 0;
     const size_t sb = codec == BHG_CODEC_SNAPPY ? bhg::scan_scratch_bytes(n) : 0;
     const size_t lb = codec == BHG_CODEC_SNAPPY && out_vals ? bhg::snappy_list_bytes(n) : 0;
-    const size_t mb = lb ? (size_t)n * 4 : 0, pb = lb ? bhg::snappy_ops_bytes(n) : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     if (int r = ensure_buf(c, &c->h_src, &c->h_src_cap, src_len + 64)) return r;
-    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap,
-                           al(hb) + al(db) + al(eb) + al(ob) + al(sb) + al(lb) + al(mb) + al(pb) + 256))
-        return r;
+    if (int r = ensure_buf(c, &c->h_aux, &c->h_aux_cap, al(hb) + al(db) + al(eb) + al(ob) + al(sb) + al(lb) + 256)) return r;
     uint8_t *a = reinterpret_cast<uint8_t *>(c->h_aux);
     bhg_handle *dh = reinterpret_cast<bhg_handle *>(a); a += al(hb);
     bhg_desc *dd = reinterpret_cast<bhg_desc *>(a); a += al(db);
     uint32_t *de = expected_crc ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(eb);
     uint64_t *doff = ob ? reinterpret_cast<uint64_t *>(a) : nullptr; a += al(ob);
     void *dscan = sb ? a : nullptr; a += al(sb);
-    uint32_t *dlist = lb ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(lb);
-    uint32_t *dmeta = mb ? reinterpret_cast<uint32_t *>(a) : nullptr; a += al(mb);
-    uint16_t *dops = pb ? reinterpret_cast<uint16_t *>(a) : nullptr;
+    uint32_t *dlist = lb ? reinterpret_cast<uint32_t *>(a) : nullptr;
     hipStream_t s = c->stream;
     HIP_TRY(c, hipMemcpyAsync(c->h_src, src, src_len, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(dh, handles, hb, hipMemcpyHostToDevice, s));
     if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc, eb, hipMemcpyHostToDevice, s));
     bhg::Launch L = launch_of(c, nullptr);
     const uint8_t *dsrc = reinterpret_cast<const uint8_t *>(c->h_src);
-    if (codec == BHG_CODEC_NONE) {
-        HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, de, dd));
-    } else {
-        if (dlist) HIP_TRY(c, hipMemsetAsync(dlist, 0, 4, s));
-        HIP_TRY(c, bhg::launch_snappy_front(L, dsrc, src_len, dh, n, de, dd, doff, dmeta, dops, dlist));
+    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, codec, de, dd, doff));
+    if (codec == BHG_CODEC_SNAPPY) {
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, doff, doff, n, dscan));
         HIP_TRY(c, hipMemcpyAsync(out_val_off, doff, ob, hipMemcpyDeviceToHost, s));
         HIP_TRY(c, hipStreamSynchronize(s));
@@ -487,7 +476,7 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
             if (total > out_vals_cap) total = out_vals_cap;
             if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 64)) return r;
             uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals);
-            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dmeta, dops, dlist));
+            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dlist));
             if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
         }
     }

@@ -6,9 +6,11 @@
 //   k_crc_long                    workgroup per LONG range (the per-table
 //                                 indexhash_checksum, writer.go:476-478)
 //   launch_decode                 NoCompressor: k_decode_tile
-//                                 (bhg_decode_tile.hip); SnappyCompressor runs
-//                                 k_snappy_front -> scan -> k_snappy_mat /
-//                                 k_snappy_rt (bhg_api.hip)
+//                                 (bhg_decode_tile.hip); snappy: the header /
+//                                 CRC pass of k_decode_stream
+//                                 (bhg_decode_stream.hip), then k_snappy_rt
+//                                 (bhg_snappy_dec.hip) after the size scan
+#include "bhg_decode_stream.h"
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -110,8 +112,9 @@ __global__ __launch_bounds__(kLongThreads) void k_crc_long(const uint8_t *__rest
 // host launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                         const uint32_t *expected_crc, bhg_desc *out) {
-    return launch_decode_tile(L, src, src_len, h, n, expected_crc, out);
+                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes) {
+    if (codec == BHG_CODEC_NONE) return launch_decode_tile(L, src, src_len, h, n, expected_crc, out);
+    return launch_decode_stream(L, src, src_len, h, n, 1, expected_crc, out, sizes);
 }
 
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

@@ -1,5 +1,5 @@
-// bhg_decode_stream.h (lab only; no longer in the product) -- a NoCompressor batch decode for gfx950 (and
-// round 2's header / CRC pass of the snappy decode, replaced by k_snappy_front): readRecordHeader + readRecord +
+// bhg_decode_stream.h -- the NoCompressor batch decode for gfx950 (and the
+// header / CRC pass of the snappy decode): readRecordHeader + readRecord +
 // readKV + FNV-1 + masked CRC-32C per block (bithash/block2.go:31-66,
 // compress.go:57-59, internal/hash/fnv.go:19-23, internal/crc/crc.go:19-33).
 //
@@ -32,8 +32,8 @@
 // LDS: Crc4Perm (slice-by-4 replicated 32x, 128 KiB, conflict free) + the
 // fold table + six scan tables + E = 156.5 KiB -> one workgroup per CU.
 #pragma once
-#include "../../bitalosdb_amd/csrc/bhg_crc_tables.h"
-#include "../../bitalosdb_amd/csrc/bhg_device.h"
+#include "bhg_crc_tables.h"
+#include "bhg_device.h"
 
 namespace bhg {
 
@@ -72,8 +72,7 @@ __device__ __forceinline__ uint32_t ld32_clamp(uint64_t a, uint64_t lo4, uint64_
     return gld<uint32_t>(a < lo4 ? lo4 : (a > hi4 ? hi4 : a));
 }
 
-using bhg::wave_incl_add;
-using bhg::wave_incl_max;
+// wave_incl_add / wave_incl_max: bhg_device.h
 
 }  // namespace stream_detail
 

@@ -1,0 +1,36 @@
+// bhg_decode_stream.hip -- launcher of k_decode_stream (bhg_decode_stream.h):
+// the snappy header / CRC pass (MODE 1) of bhg_decode_batch.
+#include "bhg_decode_stream.h"
+#include "bhg_internal.h"
+
+namespace bhg {
+
+#ifndef BHG_STREAM_NCH
+#define BHG_STREAM_NCH 4
+#endif
+#ifndef BHG_STREAM_WIN
+#define BHG_STREAM_WIN 128
+#endif
+#ifndef BHG_STREAM_PIPE
+#define BHG_STREAM_PIPE 0
+#endif
+
+size_t stream_tab_words() { return kStreamTabWords; }
+void build_stream_tab_default(uint32_t *out) { build_stream_tab(out, BHG_STREAM_WIN, BHG_STREAM_NCH); }
+
+// MODE 1 only: the NoCompressor decode is k_decode_tile (MODE 0 of this kernel measured
+// slower, DESIGN.md 4.1, and stays a lab build)
+hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes) {
+    if (mode != 1) return hipErrorInvalidValue;
+    constexpr int WPB = 8;  // 156.5 KiB of LDS: one workgroup per CU
+    const uint64_t tiles = (n + 63) / 64;
+    const uint64_t need = (tiles + WPB - 1) / WPB, cap = (uint64_t)L.num_cus;
+    uint32_t grid = (uint32_t)(need < cap ? need : cap);
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((k_decode_stream<1, BHG_STREAM_NCH, WPB, BHG_STREAM_WIN, BHG_STREAM_PIPE>), dim3(grid),
+                       dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab);
+    return hipGetLastError();
+}
+
+}  // namespace bhg

@@ -81,6 +81,15 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {  // values >= 0:
     y = BHG_DPP(x, 0x143, 0xc); x = y > x ? y : x;
     return x;
 }
+__device__ __forceinline__ uint32_t wave_incl_or(uint32_t x) {
+    x |= BHG_DPP(x, 0x111, 0xf);
+    x |= BHG_DPP(x, 0x112, 0xf);
+    x |= BHG_DPP(x, 0x114, 0xf);
+    x |= BHG_DPP(x, 0x118, 0xf);
+    x |= BHG_DPP(x, 0x142, 0xa);
+    x |= BHG_DPP(x, 0x143, 0xc);
+    return x;
+}
 #undef BHG_DPP
 
 // Lanes of a wave hand LDS bytes to each other (one lane writes, another

@@ -5,7 +5,6 @@
 #include <stdint.h>
 
 #include "../../include/bithashgpu.h"
-#include "bhg_snappy_parse.h"
 
 namespace bhg {
 
@@ -13,6 +12,7 @@ struct Launch {
     hipStream_t stream;
     int num_cus;           // 256 on MI355X
     const uint32_t *ztab;  // device copy of build_tile_ztab() (owned by the context)
+    const uint32_t *stab;  // device copy of build_stream_tab(128, 4) (owned by the context)
 };
 
 // persistent grid for lane-per-item kernels: enough workgroups to fill the
@@ -44,27 +44,26 @@ inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback
     return b > 0 ? (uint32_t)b : 1u;
 }
 
-// bhg_decode.hip: the NoCompressor decode (complete descriptors)
+// bhg_decode.hip: descriptors for codec NONE (complete) or the snappy header
+// pass (sizes[i] = decoded length; the values follow with launch_snappy)
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                         const uint32_t *expected_crc, bhg_desc *out);
+                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
 // bhg_decode_tile.hip: the NoCompressor decode kernel
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out);
-// SnappyCompressor decode, three launches on one stream:
-//  1. bhg_snappy_front.hip: descriptors (provisional value fields), sizes[i] = decoded
-//     length, and -- when ops != null -- the tag walk into ops (n x kSnapOpCap u16),
-//     meta (n u32) and the fallback list (snappy_list_bytes(n), count zeroed by the caller);
-//  2. the exclusive scan of sizes -> val_off;
-//  3. bhg_snappy_dec.hip: the LDS op replay (k_snappy_mat), then k_snappy_rt over the list;
-//     meta / ops / list null -> every block through k_snappy_rt.
-hipError_t launch_snappy_front(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                               const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes, uint32_t *meta,
-                               uint16_t *ops, uint32_t *list);
+// bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
+// the shift tables it reads (Launch::stab) are built on the host once per context
+size_t stream_tab_words();
+void build_stream_tab_default(uint32_t *out);
+hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+// bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
+// list: device scratch of snappy_list_bytes(n) (the blocks the LDS decoder hands to the
+// global-memory pass); null -> every block through the global-memory kernel
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
-                         const uint32_t *meta, const uint16_t *ops, const uint32_t *list);
+                         uint32_t *list);
 inline size_t snappy_list_bytes(uint32_t n) { return 4 + 4 * (size_t)n; }
-inline size_t snappy_ops_bytes(uint32_t n) { return (size_t)n * kSnapOpCap * 2; }
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)

@@ -41,6 +41,7 @@
 // dependent element steps, not by HBM bandwidth.
 #include "bhg_device.h"
 #include "bhg_internal.h"
+#include "bhg_snappy_parse.h"
 
 namespace bhg {
 
@@ -201,180 +202,119 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
-// k_snappy_lds: lane per block, the block staged in LDS, a branch-free element
-// step, and the next group's streams prefetched into registers while this
-// group decodes.
+// k_snappy_mat: the value bytes of the blocks k_snappy_front parsed, in LDS.
 //
-// A workgroup is one wave and owns BPW LDS slots of SLOT bytes.  The block
-// decodes IN PLACE: its output grows from the slot start, its stream is staged
-// at the slot end (P = (SLOT - 8 - round16(clen)) & ~15), and the walk checks
-// before every element that its writes (which overshoot by up to 15 B) stay
-// below the next unread tag; a block that would break that (or does not fit)
-// is listed for the lane-per-block k_snappy_rt pass from global memory.  At C3
-// (1 KiB values, streams <= 721 B) a 1,088-B slot never falls back, so 144
-// blocks are resident per CU (8 waves x 18) instead of 80 with separate
-// stream and output areas (measured: 1,152-B slots x 17 blocks 1.080 ms per C3
-// step, 1,088 x 18 1.044, 1,088 x 17 1.077, 1,072 x 19 1.178).  Per group of BPW consecutive blocks:
+// A workgroup is one wave and owns kSnapBPW slots of kSnapSlot bytes, lane b
+// = block b of a group of kSnapBPW consecutive blocks.  A block decodes IN
+// PLACE in its slot: the compressed stream staged at the slot end (P =
+// slot_stream_pos(clen)), the output growing from the slot start.  The tag
+// walk is already done (bhg_snappy_parse.h): the lane replays the block's ops,
+// each one 16-B LDS read + one 16-B LDS write, read from the op scratch 8 at a
+// time (two 16-B chunks in flight).  Per group:
 //   1. the group's streams (prefetched into VGPRs, one 16-B chunk per lane per
 //      block) are written into the slots;
 //   2. the NEXT group's streams are requested (loads in flight during 3-5),
 //      and the descriptors of the group after it;
-//   3. lane b walks block b entirely in LDS;
+//   3. lane b replays block b's ops (status TOO_LARGE / a corrupt stream: no ops);
 //   4. the wave stores each decoded block with contiguous 16-B stores;
 //   5. the descriptors are finalised.
-// The element step moves every element as "ops" of 16 B (84 % of C3 elements
-// are <= 16 B), one 16-B read and one 16-B write, no masking:
-//   literal, or copy of offset o >= 16:  op j reads src + 16 j, writes d + 16 j
-//     (a copy's source of op j lies below d + 16 j: written by ops < j)
-//   copy of offset o < 16:  op t reads the 16 B at d - o (its first o bytes
-//     valid), writes them at d + t o
-// A write past the element's end lands in bytes later elements (or the pad)
-// own and is overwritten by them in program order; for a short-offset copy
-// the last write to every byte comes from the op whose period holds it (LDS
-// is in order per wave, so a read sees every earlier write of its lane).  So
-// every byte of [0, dlen) ends up right, and a typical element is one op with
-// the next tag's read in flight alongside it.  (64-B ops measured 18 % slower:
-// 4x the LDS bytes, and unaligned LDS accesses stall -- PMC: 55 % of LDS-active
-// cycles; dword-aligned stores with a read-back head merge measured 21 % slower.)
-// Checks are the reference decoder's, as in snappy_decode_rt.
+// 8 waves per CU (two per SIMD) x 18 slots of 1,088 B fill the 160 KiB of LDS.
+// Blocks the front pass could not take (oversize, in-place spill, op cap) were
+// listed for k_snappy_rt, launched after this kernel.
 // ---------------------------------------------------------------------------
-#ifndef BHG_SNAPPY_LDS
-#define BHG_SNAPPY_LDS 1
-#endif
-#ifndef BHG_SL_BPW
-#define BHG_SL_BPW 18
-#endif
-#ifndef BHG_SL_SLOT
-#define BHG_SL_SLOT 1088
-#endif
-
-// Every LDS access of k_snappy_lds goes through these may_alias types: the slot
-// is written as 16-B chunks and read as bytes, 8-B tags and 16-B chunks, and
-// type-based alias analysis must not reorder those accesses.
-typedef uint64_t u64_lds_u __attribute__((aligned(1), may_alias));
 typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));
-
 
 namespace {
 
-// Lanes of the wave hand LDS bytes to each other (staging -> walk -> store-out
-// -> next staging): LDS runs a wave's accesses in program order, but the
-// compiler sees one thread and could move a read above another lane's write,
-// so each hand-over is a wavefront-scope fence.
-__device__ __forceinline__ void sl_wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
+// mode of a block in k_snappy_mat
+enum : uint32_t { SM_SKIP = 0, SM_LDS = 1, SM_FINAL = 2 };
 
-// mode of a block in k_snappy_lds
-enum : uint32_t { SL_SKIP = 0, SL_LDS = 1, SL_GLOBAL = 2, SL_TOOLARGE = 3 };
-
-struct SlInfo {
+struct MatInfo {
     uint64_t cp, o0;  // stream (absolute, varint header included), output offset in out_vals
-    uint32_t clen, dlen, status, mode;
+    uint32_t clen, dlen, status, mode, nops;
 };
 
-// in-place slot: where a stream of clen bytes is staged (16-B aligned, 8 B of
-// tag over-read room after it)
-template <int SLOT>
-__device__ __forceinline__ uint32_t sl_pos(uint32_t clen) {
-    return ((uint32_t)SLOT - 8u - ((clen + 15u) & ~15u)) & ~15u;
-}
-
 // All loads first and unconditional (index clamped to n - 1), so the caller can
-// issue them ahead of the stream prefetch and wait for them alone (vmcnt is in
-// order: a wait for a load issued after the prefetch would wait for it too).
-template <int SLOT>
-__device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
-                                          const uint64_t *val_off, uint64_t base, uint64_t out_cap) {
+// issue them ahead of the stream prefetch and wait for them alone.
+__device__ __forceinline__ MatInfo mat_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
+                                            const uint64_t *val_off, const uint32_t *meta, uint64_t base,
+                                            uint64_t out_cap) {
     const uint32_t ii = i < n ? i : n - 1;
     const uint32_t *dw = reinterpret_cast<const uint32_t *>(out + ii);
     const uint32_t st = dw[9];
-    const uint32_t cpos = dw[2], dlen = dw[3];  // provisional (header pass): value position in the record, decoded length
+    const uint32_t cpos = dw[2], dlen = dw[3];  // provisional (front pass): value position in the record, decoded length
     const bhg_handle h = handles[ii];
     const uint64_t o0 = val_off[ii], o1 = val_off[ii + 1];
-    SlInfo r;
+    const uint32_t m = meta[ii];
+    MatInfo r;
     r.cp = base + h.offset + cpos;
     r.o0 = o0;
     r.clen = h.length - cpos;
     r.dlen = dlen;
+    r.nops = m >> 8;
     r.status = st;
-    if (i >= n || (st != BHG_ST_OK && st != BHG_ST_CRC_MISMATCH))
-        r.mode = SL_SKIP;
-    else if (o1 > out_cap || o1 - o0 < dlen)
-        r.mode = SL_TOOLARGE;
-    else
-        r.mode = (dlen <= 1024u && r.clen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
-    return r;
-}
-
-// block staged in LDS: tag stream [sp, se), output at op (LDS byte addresses,
-// op < sp: in place).  Returns 0 (ok), 1 (snappy.ErrCorrupt) or 2 (an element
-// would write into the unread stream: decode the block from global memory).
-// The element decode is straight-line (selects, non-short-circuit checks) so
-// the 64 lanes of a wave do not split into per-tag-type paths; the tag read is
-// unconditional (a read at se lies inside the slot).
-__device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op,
-                                                    uint32_t dlen) {
-    uint32_t s = sp, d = 0, res = 0;
-    // the tag and the 4 bytes after it (one unaligned ds_read_b64; two aligned dword reads
-    // measured no faster)
-    auto tag_at = [&](uint32_t p) -> uint64_t { return *reinterpret_cast<const u64_lds_u *>(lds + p); };
-    uint64_t t8 = tag_at(s);
-    while (s < se) {
-        const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
-        const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
-        // per-type constants from shifts of packed nibble/byte tables (straight-line; the
-        // ?: form compiled to per-type exec-mask branches):
-        //   adv: literal 1, copy-1 2, copy-2 3, copy-4 5;  offset mask: ~0 >> {-, 24, 16, 0}
-        const uint32_t mlit = 0u - (uint32_t)(ty == 0u), m1 = 0u - (uint32_t)(ty == 1u);
-        uint32_t n = (m1 & (4u + (x & 7u))) | (~m1 & (x + 1u));
-        uint32_t adv = (0x5321u >> (4u * ty)) & 0xfu;
-        const uint32_t off = (b14 & (0xffffffffu >> ((0x00101800u >> (8u * ty)) & 0xffu))) | (m1 & ((tag >> 5) << 8));
-        if (ty == 0u && x >= 60u) {  // long literal: 1-4 length bytes (rare; divergent)
-            const uint32_t nb = x - 59u;
-            const uint32_t lmask = nb >= 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u);
-            n = (b14 & lmask) + 1u;
-            adv = 1u + nb;
+    r.mode = SM_SKIP;
+    if (i < n && (m & 3u) == SNAP_LDS && (st == BHG_ST_OK || st == BHG_ST_CRC_MISMATCH)) {
+        // snappy.Decode's order: the output capacity first, then the stream (decode_other.go)
+        if (o1 > out_cap || o1 - o0 < dlen) {
+            r.status = BHG_ST_SNAPPY_TOO_LARGE;
+            r.mode = SM_FINAL;
+        } else if (m & 4u) {
+            r.status = BHG_ST_SNAPPY_CORRUPT;
+            r.mode = SM_FINAL;
+        } else {
+            r.mode = SM_LDS;
         }
-        const uint32_t rem = se - s;  // >= 1
-        // checks of decode_other.go (n == 0 only for a 4-byte literal length of 2^32 - 1: too long)
-        const uint32_t bad_lit = (uint32_t)(n > rem - adv), bad_cp = (uint32_t)(off == 0u) | (uint32_t)(off > d);
-        const bool bad = ((uint32_t)(adv > rem) | (uint32_t)(n > dlen - d) | (uint32_t)(n == 0u) |
-                          (mlit & bad_lit) | (~mlit & bad_cp)) != 0u;
-        const uint32_t sn = s + adv + (mlit & n);
-        const bool spill = op + d + n + 16u > sn;  // 16-B ops write below op + d + n + 16; the next tag is at sn
-        if (bad | spill) {
-            res = bad ? 1u : 2u;
-            break;
-        }
-        const uint64_t t8n = tag_at(sn);  // next tag, in flight
-        const uint32_t a = (mlit & (s + adv)) | (~mlit & (op + d - off));
-        const uint32_t o = op + d;
-        // 16-B ops (84 % of C3 elements are <= 16 B): a literal or a copy of offset >= 16 moves
-        // 16 B at a time (a copy's op j reads bytes below o + 16 j, written by ops < j); a copy of
-        // offset < 16 writes the 16 B at a (its first `off` bytes valid) at o, o + off, ...
-        const uint32_t big = mlit | (0u - (uint32_t)(off >= 16u));
-        const uint32_t sstep = big & 16u;
-        const uint32_t dstep = (big & 16u) | (~big & off);
-        for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep)
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
-        d += n;
-        s = sn;
-        t8 = t8n;
     }
-    return res ? res : (d == dlen ? 0u : 1u);
+    return r;
 }
 
 }  // namespace
 
+// Op replay with dword-aligned LDS accesses only: a 16-B (or 8-B) LDS access
+// off its natural alignment is replayed at 64 cycles per instruction on gfx950,
+// and op sources / destinations sit at any byte.  An op reads the 5 dwords
+// around its source and assembles the 16 bytes with v_perm; it writes 5 dwords
+// from its destination's dword, the first merged with the lane's copy of that
+// dword's final bytes (pend) -- so nothing is read back.  Writes reach 20 B past
+// the cursor (k_snappy_front's in-place margin).
+typedef uint32_t u32_lds __attribute__((may_alias));
+
 template <int BPW, int SLOT>
-__global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
+__device__ __forceinline__ void mat_replay_op(uint8_t *lds, uint32_t op, bool act, uint32_t slot0, uint32_t trash,
+                                              uint32_t &d, uint32_t &pend) {
+    u32_lds *L = reinterpret_cast<u32_lds *>(lds);
+    const uint32_t src = act ? slot0 + (op & 0x7ffu) : slot0;
+    const uint32_t len = (op >> 11) + 1u;
+    const uint32_t as = src >> 2, sr = src & 3u;
+    const uint32_t r0 = L[as], r1 = L[as + 1], r2 = L[as + 2], r3 = L[as + 3], r4 = L[as + 4];
+    const uint32_t selr = 0x03020100u + sr * 0x01010101u;
+    const uint32_t b0 = __builtin_amdgcn_perm(r1, r0, selr), b1 = __builtin_amdgcn_perm(r2, r1, selr);
+    const uint32_t b2 = __builtin_amdgcn_perm(r3, r2, selr), b3 = __builtin_amdgcn_perm(r4, r3, selr);
+    const uint32_t sh = d & 3u;                                    // slot0 is 16-B aligned
+    const uint32_t selw = 0x07060504u - sh * 0x01010101u;          // bytes [4 - sh, 8 - sh) of (hi:lo)
+    const uint32_t m = (1u << (8u * sh)) - 1u;                     // the sh final bytes of pend
+    const uint32_t sel0 = (0x03020100u & m) | (selw & ~m);
+    const uint32_t q0 = __builtin_amdgcn_perm(b0, pend, sel0), q1 = __builtin_amdgcn_perm(b1, b0, selw);
+    const uint32_t q2 = __builtin_amdgcn_perm(b2, b1, selw), q3 = __builtin_amdgcn_perm(b3, b2, selw);
+    const uint32_t q4 = __builtin_amdgcn_perm(b3, b3, selw);
+    const uint32_t D = (act ? slot0 + d : trash) >> 2;
+    L[D] = q0; L[D + 1] = q1; L[D + 2] = q2; L[D + 3] = q3; L[D + 4] = q4;
+    const uint32_t jn = (sh + len) >> 2;                           // the dword holding the new cursor
+    const uint32_t pn = jn == 0 ? q0 : jn == 1 ? q1 : jn == 2 ? q2 : jn == 3 ? q3 : q4;
+    pend = act ? pn : pend;
+    d += act ? len : 0u;
+}
+
+template <int BPW, int SLOT>
+__global__ __launch_bounds__(64) void k_snappy_mat(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off,
-                                                   uint32_t *__restrict__ list) {
-    static_assert(SLOT % 16 == 0, "16-B aligned slots");
+                                                   const uint32_t *__restrict__ meta,
+                                                   const uint16_t *__restrict__ ops) {
+    static_assert(SLOT % 16 == 0 && BPW <= 64, "16-B aligned slots, a lane per block");
+    constexpr uint32_t kChunks = kSnapOpCap / 8, kRegChunks = 12;  // 16-B op chunks; the first 96 ops ride in VGPRs
     __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
@@ -382,23 +322,27 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
-    auto info = [&](uint32_t grp) -> SlInfo {
+    auto info = [&](uint32_t grp) -> MatInfo {
         const uint32_t i = grp * BPW + lane;
-        SlInfo r = sl_info<SLOT>(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, base, out_cap);
-        return r;
+        return mat_info(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, meta, base, out_cap);
+    };
+    auto op_chunks = [&](uint32_t grp) -> const u32x4 * {
+        const uint32_t i = grp * BPW + (lane < BPW ? lane : 0u);
+        return reinterpret_cast<const u32x4 *>(ops + (uint64_t)(i < n ? i : n - 1) * kSnapOpCap);
     };
     u32x4 v[BPW];
+    u32x4 opc[kRegChunks], opn[kRegChunks];
     // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
     // past the stream load src + 0; the dump drops them) and clamped to end
     // src (a chunk that would cross the end is loaded from end - 16 and
     // shifted into place at the dump), so no branch and no wait is tied to the
     // loads until the next dump.  (The launcher sends src_len < 64 elsewhere.)
-    auto chunk_addr = [&](const SlInfo &I, int b, uint32_t &clb) -> uint64_t {
-        clb = __builtin_amdgcn_readlane(I.mode == SL_LDS ? I.clen : 0u, b);
+    auto chunk_addr = [&](const MatInfo &I, int b, uint32_t &clb) -> uint64_t {
+        clb = __builtin_amdgcn_readlane(I.mode == SM_LDS ? I.clen : 0u, b);
         const uint64_t cpb = readlane_u64(I.cp, b);
         return 16 * lane < clb ? cpb + 16 * lane : base;
     };
-    auto prefetch = [&](const SlInfo &I) {
+    auto prefetch = [&](const MatInfo &I) {
 #pragma unroll
         for (int b = 0; b < BPW; b++) {
             uint32_t clb;
@@ -406,11 +350,18 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             v[b] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
         }
     };
-    SlInfo cur = info(g);
+    auto load_ops = [&](u32x4 (&dst)[kRegChunks], uint32_t grp) {
+        const u32x4 *oc = op_chunks(grp < ngroups ? grp : g);
+#pragma unroll
+        for (uint32_t c = 0; c < kRegChunks; c++) dst[c] = oc[c];
+    };
+    MatInfo cur = info(g);
+    load_ops(opc, g);
     prefetch(cur);
-    SlInfo nxt = info(g + G);
+    MatInfo nxt = info(g + G);
     for (; g < ngroups; g += G) {
-        // 1. this group's streams -> slots
+        // 1. this group's streams -> slots (the wait here also covers this group's op chunks,
+        //    loaded before the streams)
 #pragma unroll
         for (int b = 0; b < BPW; b++) {
             uint32_t clb;
@@ -423,30 +374,41 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
                 x >>= 8 * sh;
                 c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
             }
-            if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 16 * lane) = c;
+            if (16 * lane < clb)
+                *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + slot_stream_pos(SLOT, clb) + 16 * lane) = c;
         }
-        sl_wsync();
-        // 2. descriptors of the group after next, then the next group's streams in flight
-        const SlInfo nn = info(g + 2 * G);
+        lds_wave_sync();
+        // 2. descriptors of the group after next; the next group's op chunks, then its streams, in flight
+        const MatInfo nn = info(g + 2 * G);
+        load_ops(opn, g + G);
         prefetch(nxt);
-        // 3. decode
-        uint32_t fin = cur.status, mode = cur.mode;
-        if (mode == SL_LDS) {
-            const uint32_t sb = lane * SLOT, sp = sb + sl_pos<SLOT>(cur.clen);
-            uint32_t hdr = 0;
-            while (hdr < 5 && lds[sp + hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
-            hdr++;
-            const uint32_t r = snappy_walk_lds(lds, sp + hdr, sp + cur.clen, sb, cur.dlen);
-            if (r == 1) fin = BHG_ST_SNAPPY_CORRUPT;
-            if (r == 2) mode = SL_GLOBAL;
-        } else if (mode == SL_TOOLARGE) {
-            fin = BHG_ST_SNAPPY_TOO_LARGE;
+        // 3. replay the ops (8 per 16-B chunk): the first kRegChunks chunks from VGPRs, the rest loaded here
+        const uint32_t nops = cur.mode == SM_LDS ? cur.nops : 0u;
+        const uint32_t nch = (nops + 7) >> 3;
+        const uint32_t maxc = __builtin_amdgcn_readlane(wave_incl_max(nch), 63);
+        if (lane < BPW && maxc) {
+            const uint32_t slot0 = lane * SLOT, trash = slot0 + SLOT - 32;
+            uint32_t d = 0, pend = 0;
+            auto replay8 = [&](const u32x4 &w, uint32_t c) {
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) {
+                    const uint32_t word = j < 2 ? w.x : j < 4 ? w.y : j < 6 ? w.z : w.w;
+                    mat_replay_op<BPW, SLOT>(lds, (word >> (16 * (j & 1))) & 0xffffu, 8 * c + j < nops, slot0, trash,
+                                             d, pend);
+                }
+            };
+#pragma unroll
+            for (uint32_t c = 0; c < kRegChunks; c++)
+                if (c < maxc) replay8(opc[c], c);
+            if (maxc > kRegChunks) {
+                const u32x4 *oc = op_chunks(g);
+                for (uint32_t c = kRegChunks; c < maxc && c < kChunks; c++) replay8(oc[c], c);
+            }
         }
         // 4. decoded blocks -> out_vals
-        sl_wsync();
+        lds_wave_sync();
         {
-            const bool good = mode == SL_LDS && (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH);
-            const uint32_t dl = good ? cur.dlen : 0u;
+            const uint32_t dl = cur.mode == SM_LDS ? cur.dlen : 0u;
 #pragma unroll
             for (int b = 0; b < BPW; b++) {
                 const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
@@ -457,43 +419,41 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
                 }
             }
         }
-        sl_wsync();
-        // 5. descriptors (SL_GLOBAL blocks stay provisional, listed for the k_snappy_rt pass)
-        if (mode == SL_GLOBAL) {
-            const uint32_t k = atomicAdd(list, 1u);
-            list[1 + k] = g * BPW + lane;
-        }
-        if (mode == SL_LDS || mode == SL_TOOLARGE) {
+        lds_wave_sync();
+        // 5. descriptors
+        if (cur.mode != SM_SKIP) {
             uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
+            const bool ok = cur.status == BHG_ST_OK || cur.status == BHG_ST_CRC_MISMATCH;
             dw[2] = 0;
-            dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? cur.dlen : 0u;
-            dw[9] = fin;
+            dw[3] = ok ? cur.dlen : 0u;
+            dw[9] = cur.status;
         }
         cur = nxt;
         nxt = nn;
+#pragma unroll
+        for (uint32_t c = 0; c < kRegChunks; c++) opc[c] = opn[c];
     }
 }
 
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
-                         uint32_t *list) {
-    if (BHG_SNAPPY_LDS && src_len >= 64 && list) {
-        if (hipError_t e = hipMemsetAsync(list, 0, 4, L.stream)) return e;
-        constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
+                         const uint32_t *meta, const uint16_t *ops, const uint32_t *list) {
+    if (src_len >= 64 && meta && ops && list) {
+        constexpr uint32_t BPW = kSnapBPW, SLOT = kSnapSlot;
         // resident workgroups per CU (LDS-bound: 8 at 18 x 1,088 B); a grid past that would
         // start its extra workgroups only when the first ones finish
         static const uint32_t per_cu =
-            resident_per_cu((const void *)k_snappy_lds<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
+            resident_per_cu((const void *)k_snappy_mat<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
         const uint32_t groups = (n + BPW - 1) / BPW;
         const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
         uint32_t grid = groups < cap ? groups : cap;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                           out_vals, out_cap, val_off, list);
+        hipLaunchKernelGGL((k_snappy_mat<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+                           out_vals, out_cap, val_off, meta, ops);
         if (hipError_t e = hipGetLastError()) return e;
-        // then the blocks it listed (too big for a slot), lane per block from global memory
+        // then the blocks the front pass listed (too big for a slot, spill, op cap), lane per block from global memory
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
-                           out_cap, val_off, (const uint32_t *)list);
+                           out_cap, val_off, list);
         return hipGetLastError();
     }
     uint32_t grid = (n + 255) / 256;

@@ -14,7 +14,7 @@
 #include <random>
 #include <vector>
 
-#include "bhg_decode_stream.h"
+#include "../../bitalosdb_amd/csrc/bhg_decode_stream.h"
 #include "../../include/bithashgpu.h"
 
 #define CK(x)                                                                              \
