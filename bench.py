@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--codec", default="none", choices=["none", "snappy"], help="c5 only")
     ap.add_argument("--c5-tables", type=int, default=184, help="c5 corpus size in 128 MiB tables")
     ap.add_argument("--no-c5", action="store_true", help="N=1: skip the nested strong_c5 record")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the two rocprofv3 --pmc child passes that measure roofline.traffic (N=1, rank 0)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "scan", "scanmix", "get",
                                                        "indexcrc"],
                     help="c1: 100k blocks on the host CPU; c2: uncompressed decode (BASELINE metric; at N > 1 "
@@ -105,16 +107,90 @@ def copy_ceiling(src_t, dev, reps=5):
     return 2.0 * src_t.numel() / (ms * 1e-3) / 1e9, ms
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the decode kernel from the committed rocprofv3
-    --pmc summary (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, KiB -> bytes)."""
-    p = os.path.join(ROOT, "profiles", "pmc_decode_c2.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        return float(json.load(open(p))["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+# HBM traffic of a config's kernels, measured in the run: bench.py starts itself again (a child
+# process; nothing is exec'd) under rocprofv3 --pmc for two short passes (the counter blocks do
+# not fit one pass) and reads the L2->fabric request counters split by request size.  gfx950's
+# FETCH_SIZE tallies 128-B requests at 64 B (MI355X_MICROARCH.md, HBM section); the split counters
+# need no correction: read = 32 n32 + 64 n64 + 128 n128, write = 32 (n - n64) + 64 n64.
+PMC_PASSES = (("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"),
+              ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"))
+
+
+def measure_traffic(config_args, kernels, timeout_s=240):
+    """{kernel prefix: median HBM bytes per launch (read, write)} from two rocprofv3 --pmc passes of
+    `bench.py <config_args> --steps 2 --warmup 1`; None (with the reason) when the profiler is
+    missing or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if prof is None:
+        return None, "rocprofv3 not found"
+    env = dict(os.environ, BHG_TRAFFIC_CHILD="1", TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    per = {}   # (kernel, dispatch) -> {counter: value}
+    names = {}
+    with tempfile.TemporaryDirectory(prefix="bhg_pmc_", dir=env["TMPDIR"]) as td:
+        for i, counters in enumerate(PMC_PASSES):
+            out = os.path.join(td, "p%d" % i)
+            cmd = [prof, "--pmc", *counters, "-d", out, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.join(ROOT, "bench.py"), *config_args, "--steps", "2", "--warmup", "1",
+                   "--no-cpu", "--no-e2e", "--no-c5"]
+            import signal
+            errf = os.path.join(td, "p%d.err" % i)
+            with open(errf, "wb") as ef:
+                pr = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=ef, start_new_session=True)
+                try:
+                    rc = pr.wait(timeout=timeout_s)
+                except subprocess.TimeoutExpired:
+                    os.killpg(pr.pid, signal.SIGKILL)    # the profiler and the bench under it
+                    pr.wait()
+                    return None, "pmc pass %d timed out" % i
+            if rc != 0:
+                return None, "pmc pass %d exit %d: %s" % (i, rc, open(errf, "rb").read()[-200:].decode(errors="replace"))
+            for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
+                for row in csv.DictReader(open(f)):
+                    kn = row["Kernel_Name"]
+                    hit = [k for k in kernels if k in kn]
+                    if not hit:
+                        continue
+                    key = (hit[0], i, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+                    per.setdefault(key, {})[row["Counter_Name"]] = float(row["Counter_Value"])
+                    names[hit[0]] = kn.split("(")[0]
+    res = {}
+    for k in kernels:
+        rd = [32 * c.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) +
+              128 * c.get("TCC_EA0_RDREQ_128B_sum", 0) for (kk, i, _), c in per.items() if kk == k and i == 0]
+        wr = [32 * (c.get("TCC_EA0_WRREQ_sum", 0) - c.get("TCC_EA0_WRREQ_64B_sum", 0)) +
+              64 * c.get("TCC_EA0_WRREQ_64B_sum", 0) for (kk, i, _), c in per.items() if kk == k and i == 1]
+        if rd and wr:
+            res[k] = {"read": float(np.median(rd)), "write": float(np.median(wr)), "launches": min(len(rd), len(wr)),
+                      "name": names.get(k, k)}
+    if not res:
+        return None, "no dispatch of %s in the pmc passes" % ",".join(kernels)
+    return res, None
+
+
+def traffic_fields(cfg_args, kernels, alg_bytes_per_launch, what):
+    """roofline.traffic (+ ratio and provenance) for the dominant kernel(s): summed per-launch
+    bytes of `kernels` from measure_traffic; null with the reason when not measurable."""
+    if os.environ.get("BHG_TRAFFIC_CHILD") or os.environ.get("BHG_NO_TRAFFIC"):
+        return {"traffic": None, "traffic_source": "not measured (profiling child or BHG_NO_TRAFFIC)"}
+    res, err = measure_traffic(cfg_args, kernels)
+    if res is None:
+        return {"traffic": None, "traffic_source": "not measured: %s" % err}
+    tot = sum(v["read"] + v["write"] for v in res.values())
+    return {"traffic": round(tot), "traffic_ratio": round(tot / alg_bytes_per_launch, 4),
+            "traffic_source": "measured in this run: bench.py %s under rocprofv3 --pmc (%s | %s), median per "
+                              "launch of %s; HBM bytes = 32/64/128-B read requests + 32/64-B write requests at "
+                              "the L2 fabric interface; algorithmic bytes per launch %d (%s)" % (
+                                  " ".join(cfg_args), " ".join(PMC_PASSES[0]), " ".join(PMC_PASSES[1]),
+                                  ", ".join(v["name"] for v in res.values()), alg_bytes_per_launch, what),
+            "traffic_by_kernel": {v["name"]: {"read": round(v["read"]), "write": round(v["write"]),
+                                              "launches": v["launches"]} for v in res.values()}}
 
 
 BACKEND = "nccl"
@@ -340,7 +416,12 @@ def c2_measure(a, world, rank, local, dev, codec, with_extras):
     total_blocks = n_total * a.steps
     value = total_blocks * L / elapsed / 2 ** 30
     achieved = n * (ALGO_BYTES_PER_BLOCK + 4) / (avg_kern_ms * 1e-3) / 1e9   # + the expected CRC read
-    traffic = pmc_traffic()
+    if rank == 0 and world == 1 and with_extras and not a.no_traffic:
+        tf = traffic_fields(["--config", "c2", "--blocks", str(n)], ["k_decode_tile"],
+                            n * (ALGO_BYTES_PER_BLOCK + 4), "handle 16 + record %d + descriptor 40 + expected CRC 4 "
+                            "per block" % L)
+    else:
+        tf = {"traffic": None, "traffic_source": "measured only at N=1 on rank 0"}
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -359,9 +440,7 @@ def c2_measure(a, world, rank, local, dev, codec, with_extras):
                    "blocks_per_gpu": n, "record_bytes": L, "tables_per_gpu": meta["tables"],
                    "codec": "none", "parallelism": "table-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "traffic_source": "not measured in this run: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of "
-                                       "the same command, committed in profiles/pmc_decode_c2.json (k_decode_tile<8, 2>, scripts/profile_bench.sh)",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), **tf,
                      "kernel": "k_decode_tile<8, 2>", "kernel_avg_ms": round(avg_kern_ms, 4),
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK + 4,
                      "measured_copy_ceiling": {"GBps": round(copy_gbps, 1), "ms": round(copy_ms, 4),
@@ -587,8 +666,12 @@ def run_c3(a, world, rank, local, dev, codec):
     alg = n * (16 + 40 + 1024) + disk
     out["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "traffic": None, "scope": "whole step (k_snappy_front + size scan + k_snappy_mat + k_snappy_rt)",
+                       "traffic": None, "scope": "whole step (k_decode_stream<1> header/CRC pass + size scan + k_snappy_lds + k_snappy_rt)",
                        "step_event_ms": round(kms, 4)}
+    if rank == 0 and world == 1 and not a.no_traffic:
+        out["roofline"].update(traffic_fields(["--config", "c3", "--blocks", str(n)],
+                                              ["k_decode_stream", "k_snappy_lds", "k_snappy_rt"], int(alg),
+                                              "handle 16 + on-disk record + descriptor 40 + 1 KiB value per block"))
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         host = src.cpu().numpy()
@@ -644,6 +727,13 @@ def run_c4(a, world, rank, local, dev, codec):
                        "scope": "whole step (sizes, scan, k_snappy_enc, split, pack, crc)",
                        "step_event_ms": round(kms, 4),
                        "note": "k_snappy_enc is latency bound (DESIGN.md 4.3); snappy scratch traffic excluded"}
+    if rank == 0 and world == 1 and not a.no_traffic:
+        res["roofline"].update(traffic_fields(["--config", "c4", "--blocks", str(n)],
+                                              ["k_enc_sizes", "k_snappy_enc", "k_enc_split", "k_enc_tsize",
+                                               "k_enc_pack", "k_enc_crc"], int(alg),
+                                              "key + value + 16 B in, records + handle/FNV/CRC out per pair; the "
+                                              "snappy scratch written by k_snappy_enc and read by k_enc_pack is "
+                                              "extra traffic"))
     if rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         vo = val_off.cpu().numpy().astype(np.uint64)

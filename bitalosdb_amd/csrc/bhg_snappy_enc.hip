@@ -59,11 +59,12 @@ __constant__ SkipTab kSkip = SkipTab();
 
 __device__ __forceinline__ uint32_t se_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
 
-// one (unaligned) ds_read_b32: gfx950 LDS takes unaligned dword reads
-typedef uint32_t u32_lds_u __attribute__((aligned(1), may_alias));
-// (4 byte reads measured 5 % slower, two aligned dwords + a funnel shift the same)
-__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *b, uint32_t i) {
-    return *reinterpret_cast<const u32_lds_u *>(b + i);
+// in[p .. p + 4) from two dword-aligned LDS reads (one ds_read2_b32) and a byte funnel:
+// misaligned DS accesses are replayed on gfx950 (62 % of the LDS-active cycles of the
+// round-2 encoder were unaligned stalls)
+__device__ __forceinline__ uint32_t ld32a(const uint32_t *in32, uint32_t p) {
+    const uint32_t w = p >> 2;
+    return __builtin_amdgcn_alignbyte(in32[w + 1], in32[w], p & 3);
 }
 // lane i's value for a wave-uniform i: v_readlane, not an LDS permute
 __device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
@@ -122,6 +123,92 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // order LDS accesses of this wave (no instruction: LDS executes a wave's ops in order)
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
+// The matcher does not write output bytes.  Every copy it finds becomes one op --
+// (copy start, length of the literal run before it, copy length, offset), the block's
+// final literal an op with copy length 0 -- written into lane n of two VGPRs by a
+// select (no exec-mask branch, nothing on the dependency chain).  Every 64 ops
+// se_flush turns them into golang/snappy's bytes with all lanes at once: per-op sizes
+// (emitLiteral header + literal + emitCopy tags), a wave prefix sum for the output
+// offsets, tags written by their own lanes, literal bytes copied from the LDS block by
+// the whole wave.
+struct OpRing {
+    uint32_t a;  // lane k: op k's copy start | literal length << 16
+    uint32_t b;  // lane k: op k's copy length | offset << 16
+    uint32_t n;  // ops held (wave-uniform)
+};
+
+__device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, uint32_t lane) {
+    const bool act = lane < r.n;
+    const uint32_t a = act ? r.a : 0u, b = act ? r.b : 0u;
+    const uint32_t base = a & 0xffffu, lit = a >> 16, cl = b & 0xffffu, off = b >> 16;
+    const uint32_t lh = lit == 0 ? 0u : lit <= 60 ? 1u : lit <= 256 ? 2u : 3u;  // emitLiteral: n = lit - 1
+    uint32_t L = cl, n64 = 0;
+    if (L >= 68) {  // emitCopy: "for length >= 68 { 64-byte copy; length -= 64 }"
+        n64 = (L - 68) / 64 + 1;
+        L -= 64 * n64;
+    }
+    const uint32_t n60 = L > 64 ? 1u : 0u;  // "if length > 64 { 60-byte copy }"
+    if (n60) L -= 60;
+    const bool c2 = L >= 12 || off >= 2048;
+    const uint32_t ct = cl == 0 ? 0u : 3 * (n64 + n60) + (c2 ? 3u : 2u);
+    const uint32_t sz = lh + lit + ct;
+    const uint32_t incl = wave_incl_add(sz);
+    const uint32_t total = lane_val(incl, 63);
+    uint8_t *dst = o.g + o.d + (incl - sz);
+    if (lh) {
+        const uint32_t m = lit - 1;
+        dst[0] = lh == 1 ? (uint8_t)(m << 2) : lh == 2 ? (uint8_t)(60 << 2) : (uint8_t)(61 << 2);
+        if (lh >= 2) dst[1] = (uint8_t)m;
+        if (lh == 3) dst[2] = (uint8_t)(m >> 8);
+    }
+    if (cl) {
+        uint8_t *q = dst + lh + lit;
+        for (uint32_t i = 0; i < n64 + n60; i++, q += 3) {
+            q[0] = i < n64 ? (uint8_t)(63 << 2 | 2) : (uint8_t)(59 << 2 | 2);
+            q[1] = (uint8_t)off;
+            q[2] = (uint8_t)(off >> 8);
+        }
+        if (c2) {
+            q[0] = (uint8_t)((L - 1) << 2 | 2);
+            q[1] = (uint8_t)off;
+            q[2] = (uint8_t)(off >> 8);
+        } else {
+            q[0] = (uint8_t)((off >> 8) << 5 | (L - 4) << 2 | 1);
+            q[1] = (uint8_t)off;
+        }
+    }
+    // literal bytes: one op at a time, 64 bytes per wave instruction
+    uint64_t lm = __ballot(lit != 0);
+    while (lm) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(lm);
+        lm &= lm - 1;
+        const uint32_t ll = lane_val(lit, k), s0 = lane_val(base, k) - ll;
+        uint8_t *d0 = o.g + o.d + (lane_val(incl, k) - lane_val(sz, k)) + lane_val(lh, k);
+        for (uint32_t t = lane; t < ll; t += 64) d0[t] = in[s0 + t];
+    }
+    o.d += total;
+    r.n = 0;
+}
+
+__device__ __forceinline__ void se_push(Out &o, const uint8_t *in, OpRing &r, uint32_t lane, uint32_t base,
+                                        uint32_t lit, uint32_t cl, uint32_t off) {
+    const bool mine = lane == r.n;  // v_cmp + two v_cndmask: no exec-mask branch
+    r.a = mine ? base | lit << 16 : r.a;
+    r.b = mine ? cl | off << 16 : r.b;
+    if (++r.n == 64) se_flush(o, in, r, lane);
+}
+
+// First mismatch r in [0, 256) of in[c + r] vs in[s + r] (256 if all equal), 4 bytes per lane
+// from aligned reads; the caller clips it to the block end (min with len - s: bytes past len
+// are then never looked at, whatever they hold).
+__device__ __forceinline__ uint32_t se_mismatch(uint32_t A, uint32_t B) {
+    const uint32_t w = A ^ B;
+    const uint64_t mm = __ballot(w != 0);
+    if (!mm) return 256u;
+    const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+    return 4 * k + ((uint32_t)__builtin_ctz(lane_val(w, k)) >> 3);
+}
+
 // encodeBlock on an LDS-staged block (len in [17, SE_CAP]); tab zeroed by the caller.
 // this lane's skip offsets F[64 j + lane] and F[64 j + lane + 1], j < 16 (k < 1024)
 struct LaneSkip {
@@ -129,18 +216,23 @@ struct LaneSkip {
 };
 
 #ifdef BHG_SE_PROF
-__device__ uint64_t se_prof[8];  // lab: cycles in scan / literal emit / copy loop, counts
+__device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, counts
 #define SE_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
 #else
 #define SE_T(x)
 #endif
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                              const LaneSkip &F, uint64_t *acc) {
+    const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
     const uint32_t tmask = 16383;
     const uint32_t sLimit = len - SE_MARGIN;
     uint32_t nextEmit = 0, s = 1;
+    OpRing r;
+    r.a = 0;
+    r.b = 0;
+    r.n = 0;
     for (;;) {
         // ---- scan phase: iterations k = 0,1,... at positions s + F[k] ----
         uint32_t cand = 0;
@@ -163,7 +255,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // s < 64 Ki and F[k] <= 2^31 - 1: the sums fit in 32 bits
             const bool valid = s + fk1 <= sLimit;
             const uint32_t pos = valid ? s + fk : 0u;
-            const uint32_t u = lds_ld32(in, pos);
+            const uint32_t u = ld32a(in32, pos);
             const uint32_t h = se_hash(u, shift) & tmask;
             // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
             // of h mod 1024, one byte per bucket (<= 64 adds per byte)
@@ -174,6 +266,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint64_t dm0 = __ballot(maybe_dup);
             uint64_t dm = dm0;
             uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
+#ifdef BHG_SE_PROF
+            acc[6] += 1;
+            acc[7] += __builtin_popcountll(dm0);
+#endif
             while (dm) {
                 const uint32_t i = __builtin_ctzll(dm);
                 dm &= dm - 1;
@@ -182,7 +278,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             }
             atomicSub(&dcnt[slot], valid ? 1u << sh8 : 0u);
             wsync();
-            const bool eq = lds_ld32(in, c) == u;
+            const bool eq = ld32a(in32, c) == u;
             const bool m = valid && eq;
             const uint64_t ev = __ballot(!valid || m);
             const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
@@ -216,82 +312,67 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         acc[3] += 1;
 #endif
         if (remainder) break;
-        se_emit_literal(o, in + nextEmit, nullptr, s - nextEmit, lane);
-#ifdef BHG_SE_PROF
-        SE_T(t_lit1);
-        acc[1] += t_lit1 - t_scan1;
-#endif
-        // ---- copies: emit, then check for an immediate next match ----
-        // encode_other.go's inner loop with two LDS round trips per copy: the table
-        // read for currHash (its hash input comes from the lanes' registers), then one
-        // compare of in[cand + t] with in[s + t] for t < 64 that both verifies the
-        // 4-byte match and extends it (Go's extension starts at s + 4 after a verified
-        // 4-byte match: the same first mismatch).
+        // ---- copies (encode_other.go's inner loop).  Each iteration reads, at once,
+        // A = in[s + 4 lane ..), B = in[cand + 4 lane ..) -- their compare both verifies the
+        // 4-byte match (Go's load32 check; always true for the scan's match) and extends it
+        // (Go extends from s + 4 after a verified match: the same first mismatch) -- and
+        // U = in[s + lane .. + 4), whose hashes are the table slots of every position the copy
+        // can end at below s + 64.  The table is read for all of them right away: the only
+        // store between now and Go's lookup at the copy end e is tab[prevHash] = e - 1, and
+        // prevHash == currHash is resolved by a compare.  So the lookup costs no LDS round
+        // trip after the compare; copies ending at s + 64 or later take a serial lookup.
         bool to_rem = false;
-        uint32_t f;  // first mismatch of in[cand + t] vs in[s + t] (t < 64 per round)
-        uint32_t bt; // this lane's in[r0 + lane .. + 4) of the round that found f
-        {
-            const uint32_t t = lane;
-            const uint32_t bw = lds_ld32(in, s + t), a = in[cand + t], b = bw & 0xffu;  // past len: forced mismatch
-            bt = bw;
-            const uint64_t mm = __ballot(s + t >= len || a != b);
-            f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
-        }
+        uint32_t lit = s - nextEmit;
         for (;;) {
-            const uint32_t base = s;
-            uint32_t fb = f;  // mismatch relative to the round's start
-            uint32_t r0 = s;  // start of the round that found fb
-            while (fb == 64u) {  // all 64 equal: next round
-                r0 += 64;
-                const uint32_t t = lane;
-                const uint32_t bw = lds_ld32(in, r0 + t), a = in[cand + (r0 - base) + t], b = bw & 0xffu;
-                bt = bw;
-                const uint64_t mm = __ballot(r0 + t >= len || a != b);
-                fb = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
+            const uint32_t A = ld32a(in32, s + 4 * lane);
+            const uint32_t B = ld32a(in32, cand + 4 * lane);
+            const uint32_t U = ld32a(in32, s + lane);
+            const uint32_t hU = se_hash(U, shift) & tmask;
+            const uint32_t tU = tab[hU];
+            uint32_t f = min(se_mismatch(A, B), len - s);
+            if (f < 4u) {  // the chained candidate does not match: back to scanning at s + 1
+                s += 1;
+                break;
             }
-            s = r0 + fb;
-            se_emit_copy(o, base - cand, s - base, lane);
+            uint32_t r0 = s;  // start of the round that found the mismatch
+            while (f == 256u) {
+                r0 += 256;
+                f = min(se_mismatch(ld32a(in32, r0 + 4 * lane), ld32a(in32, cand + (r0 - s) + 4 * lane)), len - r0);
+            }
+            const uint32_t e = r0 + f;
+            se_push(o, in, r, lane, s, lit, e - s, s - cand);
+            lit = 0;
+            const uint32_t q = e - s;
+            s = e;
             nextEmit = s;
             if (s >= sLimit) { to_rem = true; break; }
-            // x = in[s - 1 .. s + 7): lane t of the last round holds in[r0 + t .. r0 + t + 4)
-            uint64_t x;
-            const uint32_t k = s - 1 - r0;  // lane holding in[s - 1]
-            if (s - 1 >= r0 && k + 4 < 64u) {
-                x = (uint64_t)lane_val(bt, k) | ((uint64_t)lane_val(bt, k + 4) << 32);
-            } else {
-                x = (uint64_t)lds_ld32(in, s - 1) | ((uint64_t)lds_ld32(in, s + 3) << 32);
+            uint32_t prevHash, currHash, tc;
+            if (q < 64u) {
+                prevHash = lane_val(hU, q - 1);
+                currHash = lane_val(hU, q);
+                tc = lane_val(tU, q);
+            } else {  // x = in[s - 1 .. s + 7), then Go's lookup
+                const uint32_t x0 = uni(ld32a(in32, s - 1)), x1 = uni(ld32a(in32, s + 3));
+                prevHash = se_hash(x0, shift) & tmask;
+                currHash = se_hash(x0 >> 8 | x1 << 24, shift) & tmask;
+                tc = uni(tab[currHash]);
             }
-            const uint32_t prevHash = se_hash((uint32_t)x, shift) & tmask;
-            const uint32_t currHash = se_hash((uint32_t)(x >> 8), shift) & tmask;
-            const uint32_t tc = tab[currHash];  // read before the two stores (program order); prevHash == currHash gives s - 1
             wsync();
             if (lane == 0) {
                 tab[prevHash] = (se_tab_t)(s - 1);
                 tab[currHash] = (se_tab_t)s;
             }
-            const uint32_t c = uni(prevHash == currHash ? s - 1 : tc);
+            cand = prevHash == currHash ? s - 1 : tc;
             wsync();
-            // verify in[c .. c + 4) == in[s .. s + 4) and extend in the same compare
-            {
-                const uint32_t t = lane;
-                const uint32_t bw = lds_ld32(in, s + t), a = in[c + t], b = bw & 0xffu;
-                bt = bw;
-                const uint64_t mm = __ballot(s + t >= len || a != b);
-                f = mm ? (uint32_t)__builtin_ctzll(mm) : 64u;
-            }
-            if (f < 4u) {
-                s += 1;
-                break;
-            }
-            cand = c;
         }
 #ifdef BHG_SE_PROF
         SE_T(t_cp1);
-        acc[2] += t_cp1 - t_lit1;
+        acc[2] += t_cp1 - t_scan1;
 #endif
         if (to_rem) break;
     }
-    if (nextEmit < len) se_emit_literal(o, in + nextEmit, nullptr, len - nextEmit, lane);
+    if (nextEmit < len) se_push(o, in, r, lane, len, len - nextEmit, 0, 0);
+    if (r.n) se_flush(o, in, r, lane);
 }
 
 // encodeBlock, lane 0 only, table of u16 in global scratch (blocks > SE_CAP)
@@ -347,9 +428,13 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                                                    uint32_t n, uint8_t *__restrict__ scratch, uint64_t scap,
                                                    const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
                                                    uint16_t *__restrict__ gtables) {
-    __shared__ __attribute__((aligned(16))) uint8_t in[SE_CAP + 16];
-    __shared__ __attribute__((aligned(16))) se_tab_t tab[SE_TAB];
-    __shared__ uint32_t dcnt[BHG_SE_DCNT];
+    // one LDS buffer: block (+16 zero bytes), table, dedupe counters.  The aligned reads of
+    // the copy loop reach up to 260 bytes past a position < SE_CAP: into the table, never past
+    // the buffer, and masked by the block length.
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4 + BHG_SE_DCNT];
+    uint8_t *in = reinterpret_cast<uint8_t *>(lds);
+    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP + 16) / 4);
+    uint32_t *dcnt = lds + (SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4;
     const uint32_t lane = threadIdx.x;
     for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
     LaneSkip F;
@@ -430,11 +515,12 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
 #ifdef BHG_SE_PROF
     acc[5] = __builtin_amdgcn_s_memtime() - t_k0;
     if (lane == 0)
-        for (int q = 0; q < 6; q++) atomicAdd((unsigned long long *)&se_prof[q], (unsigned long long)acc[q]);
+        for (int q = 0; q < 8; q++) atomicAdd((unsigned long long *)&se_prof[q], (unsigned long long)acc[q]);
     if (blockIdx.x == 0 && lane == 0)
-        printf("se_prof wave0: scan %llu lit %llu copy %llu phases %llu values %llu total %llu\n",
+        printf("se_prof wave0: scan %llu lit %llu copy %llu phases %llu values %llu total %llu batches %llu duplanes %llu\n",
                (unsigned long long)acc[0], (unsigned long long)acc[1], (unsigned long long)acc[2],
-               (unsigned long long)acc[3], (unsigned long long)acc[4], (unsigned long long)acc[5]);
+               (unsigned long long)acc[3], (unsigned long long)acc[4], (unsigned long long)acc[5],
+               (unsigned long long)acc[6], (unsigned long long)acc[7]);
 #endif
 }
 

@@ -446,10 +446,11 @@ def open_table(f):
                 conflict_buf=f[coff:coff + clen] if clen > 0 else None)
 
 
-def table_get(f, ukey, compressor=0):
-    """Reader.Get (reader.go:209-231)."""
+def table_get(f, ukey, compressor=0, khash=None):
+    """Reader.Get (reader.go:209-231); khash is the caller's (Bithash.Get passes FNV-1 of the
+    key, the default here; AddIkey callers may have written another)."""
     t = open_table(f)
-    v = hash_index_get64(t["index_data"], O.fnv32(ukey))
+    v = hash_index_get64(t["index_data"], O.fnv32(ukey) if khash is None else khash)
     if v is None:
         raise BithashError("ErrBhNotFound")
     off, length = v & 0xFFFFFFFF, v >> 32

@@ -151,7 +151,10 @@ def test_repack_short_ikey(codec):
     with torch.cuda.stream(codec.stream):
         src_t = as_device_bytes(src, codec.device)
         ht = handles_tensor(h, codec.device)
-        out_t, bufs = codec.repack_batch(src_t, ht, len(recs))
+        # the 5-byte ikey grows to 8 bytes on re-pack: room beyond len(src) (the default out_t is
+        # len(src), where the last record would be NO_SPACE)
+        out_t = torch.zeros(len(src) + 64, dtype=torch.uint8, device=codec.device)
+        out_t, bufs = codec.repack_batch(src_t, ht, len(recs), out_t=out_t)
         codec.sync()
     st = bufs.status.cpu().numpy().view(np.uint32)
     assert list(st) == [0] * len(recs)

@@ -264,7 +264,7 @@ def test_snappy_addresses_with_bit31_set(codec):
     """Round 2's intermittent fault, pinned: src and out_vals placed where the low
     32 bits of every device address have bit 31 set, so a sign-extending
     composition of a readlane'd address would fault or write elsewhere.  The
-    batch mixes slot-resident blocks (k_snappy_mat), in-place spill hand-overs
+    batch mixes slot-resident blocks (k_snappy_lds), in-place spill hand-overs
     and oversize / incompressible blocks (k_snappy_rt)."""
     from bitalosdb_amd.codec import handles_tensor
     rng = random.Random(31)

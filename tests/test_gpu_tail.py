@@ -265,6 +265,7 @@ def _ikey_table(codec, keys, trs, vals, khash, fn=9):
         codec.sync()
     size = int(bufs.table_size[0].item())
     t = tail.cpu().numpy()
+    stats = stats.cpu().numpy().view(np.uint32).reshape(-1, 4)     # per table: flat [4 * ntables]
     return res["out"][:size].tobytes() + t[int(off[0]):int(off[0]) + int(ln[0])].tobytes(), stats
 
 
@@ -293,7 +294,7 @@ def test_tail_conflict_block_past_one_restart(codec):
     assert got == exp
     for k in (keys[0], keys[20], keys[44]):
         last = max(i for i in range(len(keys)) if keys[i] == k)
-        assert T.table_get(got, k) == vals[last]
+        assert T.table_get(got, k, khash=khash[last]) == vals[last]
 
 
 def test_tail_one_key_under_two_khash(codec):
