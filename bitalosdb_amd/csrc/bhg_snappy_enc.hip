@@ -209,11 +209,10 @@ __device__ __forceinline__ uint32_t se_mismatch(uint32_t A, uint32_t B) {
     return 4 * k + ((uint32_t)__builtin_ctz(lane_val(w, k)) >> 3);
 }
 
-// encodeBlock on an LDS-staged block (len in [17, SE_CAP]); tab zeroed by the caller.
-// this lane's skip offsets F[64 j + lane] and F[64 j + lane + 1], j < 16 (k < 1024)
-struct LaneSkip {
-    uint32_t f[16], f1[16];
-};
+// lane i <- lane i + 1 (DPP wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
 
 #ifdef BHG_SE_PROF
 __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, counts
@@ -221,8 +220,64 @@ __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, c
 #else
 #define SE_T(x)
 #endif
+
+// The end of one scan batch (lane = one iteration of encodeBlock's candidate loop, in order):
+// candidates from the table as it was before the batch are corrected for buckets two lanes
+// of the batch share (the latest earlier lane wins -- Go stores every iteration's position
+// before the next lookup), the 4-byte checks evaluated, the first event (a match, or an
+// iteration past sLimit) found, and the table updated with the iterations up to it.
+// `eq` holds in[c .. c + 4) == u for the pre-batch c; lanes whose candidate changes are
+// re-checked.  Returns the event lane (>= nl: none in this batch).
+__device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
+                                             uint32_t nl, bool valid, uint32_t pos, uint32_t u, uint32_t h,
+                                             uint32_t &c, bool eq, bool &m, uint64_t *acc) {
+    // bucket duplicates inside the batch: per-bucket counts of h mod 1024, one byte per
+    // bucket (<= 64 adds per byte); lanes of a bucket with two or more are walked in order
+    const uint32_t slot = (h >> 2) & (BHG_SE_DCNT - 1u), sh8 = 8 * (h & 3);
+    atomicAdd(&dcnt[slot], valid ? 1u << sh8 : 0u);  // unconditional: no exec-mask branch
+    wsync();
+    const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
+    const uint64_t dm0 = __ballot(maybe_dup);
+#ifdef BHG_SE_PROF
+    acc[6] += 1;
+    acc[7] += __builtin_popcountll(dm0);
+#endif
+    uint64_t dm = dm0;
+    bool chg = false;
+    while (dm) {
+        const uint32_t i = __builtin_ctzll(dm);
+        dm &= dm - 1;
+        const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
+        if (valid && lane > i && hi == h) {   // lanes visited in increasing i: last wins
+            c = pi;
+            chg = true;
+        }
+    }
+    atomicSub(&dcnt[slot], valid ? 1u << sh8 : 0u);
+    wsync();
+    if (__ballot(chg)) eq = ld32a(in32, c) == u;
+    m = valid && eq;
+    const uint64_t ev = __ballot(lane < nl && (!valid || m));
+    const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
+    // table updates: iterations before the event, plus the event itself when it is a match;
+    // of the updating lanes with one bucket only the last one stores (plain u16 store)
+    const bool upd = valid && (lane < js || (lane == js && m));
+    bool last = upd;
+    dm = dm0 & __ballot(upd);
+    while (dm) {
+        const uint32_t i = __builtin_ctzll(dm);
+        dm &= dm - 1;
+        if (lane_val(h, i) == h && i > lane) last = false;
+    }
+    if (last) tab[h] = (se_tab_t)pos;
+    wsync();
+    return js;
+}
+
+// encodeBlock on an LDS-staged block (len in [17, SE_CAP]); tab zeroed by the caller.
+// f0 / f0n: this lane's skip offsets F[lane] and F[lane + 1] (the block's first batch).
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
-                             const LaneSkip &F, uint64_t *acc) {
+                             uint32_t f0, uint32_t f0n, uint64_t *acc) {
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
@@ -233,77 +288,55 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
     r.a = 0;
     r.b = 0;
     r.n = 0;
+    // after a copy chain ends, the copy loop's last (failed) check leaves in[s - 1 + lane ..)
+    // (U), its hash (hU) and the table entry of that hash (tU) in this lane's registers
+    bool fast = false;
+    uint32_t Uw = 0, hUw = 0, tUw = 0;
     for (;;) {
         // ---- scan phase: iterations k = 0,1,... at positions s + F[k] ----
         uint32_t cand = 0;
-        bool remainder = false;
+        bool remainder = false, found = false;
         SE_T(t_scan0);
-        for (uint32_t kb = 0;; kb += 64) {
-            // skip offsets from registers: a global load here would make the wave wait
-            // (vmcnt counts stores on gfx950) for every byte of output emitted so far
-            uint32_t fk = F.f[0], fk1 = F.f1[0];
-            if (kb != 0) {  // wave-uniform; the first batch is by far the most common
-                fk = 0x7fffffffu;
-                fk1 = 0x7fffffffu;
-#pragma unroll
-                for (uint32_t j = 1; j < 16; j++)
-                    if (kb == 64 * j) {
-                        fk = F.f[j];
-                        fk1 = F.f1[j];
-                    }
+        uint32_t kb = 0;
+        if (fast) {
+            // iterations 0..32 (F[k] = k; F[33] = 34) at s + k = lane k + 1 of the failed
+            // check: u, its hash and its pre-batch table entry need no LDS read, and the
+            // 4-byte check of that entry is issued with the duplicate count
+            const uint32_t u = lane_next(Uw), h = lane_next(hUw);
+            uint32_t c = lane_next(tUw);
+            const bool valid = lane <= 32 && s + (lane < 32 ? lane + 1 : 34u) <= sLimit;
+            const uint32_t pos = s + lane;
+            const bool eq = ld32a(in32, valid ? c : 0u) == u;
+            bool m;
+            const uint32_t js = se_batch(in32, tab, dcnt, lane, 33, valid, pos, u, h, c, eq, m, acc);
+            if (js < 33) {
+                found = true;
+                if (lane_val((uint32_t)m, js) == 0) remainder = true;
+                else { s = lane_val(pos, js); cand = lane_val(c, js); }
+            }
+            kb = 33;
+        }
+        for (; !found; kb += 64) {
+            // skip offsets: the block's first batch from registers, later ones from the
+            // constant table (a global load: it waits for the flushed output stores too)
+            uint32_t fk = f0, fk1 = f0n;
+            if (kb != 0) {
+                fk = kb + lane < 1025 ? kSkip.f[kb + lane] : 0x7fffffffu;
+                fk1 = kb + lane + 1 < 1025 ? kSkip.f[kb + lane + 1] : 0x7fffffffu;
             }
             // s < 64 Ki and F[k] <= 2^31 - 1: the sums fit in 32 bits
             const bool valid = s + fk1 <= sLimit;
             const uint32_t pos = valid ? s + fk : 0u;
             const uint32_t u = ld32a(in32, pos);
             const uint32_t h = se_hash(u, shift) & tmask;
-            // bucket duplicates inside the batch (latest earlier lane wins): per-bucket counts
-            // of h mod 1024, one byte per bucket (<= 64 adds per byte)
-            const uint32_t slot = (h >> 2) & (BHG_SE_DCNT - 1u), sh8 = 8 * (h & 3);
-            atomicAdd(&dcnt[slot], valid ? 1u << sh8 : 0u);  // unconditional: no exec-mask branch
-            wsync();
-            const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
-            const uint64_t dm0 = __ballot(maybe_dup);
-            uint64_t dm = dm0;
             uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
-#ifdef BHG_SE_PROF
-            acc[6] += 1;
-            acc[7] += __builtin_popcountll(dm0);
-#endif
-            while (dm) {
-                const uint32_t i = __builtin_ctzll(dm);
-                dm &= dm - 1;
-                const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
-                if (valid && lane > i && hi == h) c = pi;   // lanes visited in increasing i: last wins
-            }
-            atomicSub(&dcnt[slot], valid ? 1u << sh8 : 0u);
-            wsync();
             const bool eq = ld32a(in32, c) == u;
-            const bool m = valid && eq;
-            const uint64_t ev = __ballot(!valid || m);
-            const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
-            // table updates: iterations before the event, plus the event itself when it is a match
-            const bool upd = valid && (lane < js || (lane == js && m));
-#if BHG_SE_U16
-            // of the updating lanes with one bucket only the last one stores (plain u16 store)
-            bool last = upd;
-            dm = dm0 & __ballot(upd);
-            while (dm) {
-                const uint32_t i = __builtin_ctzll(dm);
-                dm &= dm - 1;
-                if (lane_val(h, i) == h && i > lane) last = false;
-            }
-            if (last) tab[h] = (se_tab_t)pos;
-#else
-            if (upd) atomicMax(&tab[h], pos);
-#endif
-            wsync();
+            bool m;
+            const uint32_t js = se_batch(in32, tab, dcnt, lane, 64, valid, pos, u, h, c, eq, m, acc);
             if (js < 64) {
-                const bool is_match = lane_val((uint32_t)m, js) != 0;
-                if (!is_match) { remainder = true; break; }
-                s = lane_val(pos, js);
-                cand = lane_val(c, js);
-                break;
+                found = true;
+                if (lane_val((uint32_t)m, js) == 0) remainder = true;
+                else { s = lane_val(pos, js); cand = lane_val(c, js); }
             }
         }
 #ifdef BHG_SE_PROF
@@ -332,6 +365,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             uint32_t f = min(se_mismatch(A, B), len - s);
             if (f < 4u) {  // the chained candidate does not match: back to scanning at s + 1
                 s += 1;
+                Uw = U;
+                hUw = hU;
+                tUw = tU;
+                fast = true;
                 break;
             }
             uint32_t r0 = s;  // start of the round that found the mismatch
@@ -437,12 +474,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
     uint32_t *dcnt = lds + (SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4;
     const uint32_t lane = threadIdx.x;
     for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
-    LaneSkip F;
-#pragma unroll
-    for (uint32_t j = 0; j < 16; j++) {
-        F.f[j] = kSkip.f[64 * j + lane];
-        F.f1[j] = kSkip.f[64 * j + lane + 1];
-    }
+    const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
     uint16_t *gt = gtables + (size_t)blockIdx.x * 16384;
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef BHG_SE_PROF
@@ -498,7 +530,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                 while (ts < 16384 && ts < blen) ts *= 2;
                 for (uint32_t t = lane; t < ts; t += 64) tab[t] = 0;
                 wsync();
-                se_block_lds(o, in, blen, tab, dcnt, lane, F, acc);
+                se_block_lds(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
             } else {
                 uint32_t d = o.d;
                 if (lane == 0) {

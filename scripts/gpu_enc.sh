@@ -13,8 +13,8 @@ tail -2 $O/pytest.txt
 timeout -k 10 240 python -u bench.py --config c4 --no-cpu --no-e2e > $O/c4_prod.json 2> $O/c4_prod.err || { tail -5 $O/c4_prod.err; exit 1; }
 echo "prod: $(cut -c1-300 $O/c4_prod.json)"
 for v in ${VARIANTS:-}; do
-  BHG_LIB_PATH=$PWD/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 240 python -u bench.py --config c4 --no-cpu --no-e2e > $O/c4_$v.json 2> $O/c4_$v.err || { tail -5 $O/c4_$v.err; exit 1; }
+  BHG_LIB_PATH=$PWD/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 240 python -u bench.py --config c4 --no-cpu --no-e2e --no-traffic > $O/c4_$v.json 2> $O/c4_$v.err || { tail -5 $O/c4_$v.err; exit 1; }
   echo "$v: $(cut -c1-300 $O/c4_$v.json)"
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 bench.py --config c4 --no-cpu --no-e2e --steps 5 --warmup 2 > $O/c4_prof.json 2> $O/c4_prof.err || { tail -5 $O/c4_prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 bench.py --config c4 --no-cpu --no-e2e --no-traffic --steps 5 --warmup 2 > $O/c4_rocprof.json 2> $O/c4_rocprof.err || { tail -5 $O/c4_rocprof.err; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp $f $O/c4_kernel_stats.csv
