@@ -221,55 +221,54 @@ __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, c
 #define SE_T(x)
 #endif
 
-// The end of one scan batch (lane = one iteration of encodeBlock's candidate loop, in order):
-// candidates from the table as it was before the batch are corrected for buckets two lanes
-// of the batch share (the latest earlier lane wins -- Go stores every iteration's position
-// before the next lookup), the 4-byte checks evaluated, the first event (a match, or an
-// iteration past sLimit) found, and the table updated with the iterations up to it.
-// `eq` holds in[c .. c + 4) == u for the pre-batch c; lanes whose candidate changes are
-// re-checked.  Returns the event lane (>= nl: none in this batch).
+// The end of one scan batch (lane = one iteration of encodeBlock's candidate loop, in order;
+// lanes >= nl are not part of it): candidates read from the table as it was before the batch
+// are corrected for buckets that two lanes share (the latest earlier lane wins -- Go stores
+// every iteration's position before the next lookup), the 4-byte checks evaluated, the first
+// event (a match, or an iteration past sLimit) found, and the table updated with the
+// iterations up to it.  `eq` holds in[c .. c + 4) == u for the pre-batch c; lanes whose
+// candidate changes are re-checked.  Returns the event lane (>= nl: none in this batch) and
+// m_js, whether it is a match.
 __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                                              uint32_t nl, bool valid, uint32_t pos, uint32_t u, uint32_t h,
-                                             uint32_t &c, bool eq, bool &m, uint64_t *acc) {
-    // bucket duplicates inside the batch: per-bucket counts of h mod 1024, one byte per
-    // bucket (<= 64 adds per byte); lanes of a bucket with two or more are walked in order
+                                             uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
+    // lanes that may share a bucket: per-bucket counts of h mod 1024, one byte per bucket
+    // (<= 64 adds per byte); only those lanes are walked
     const uint32_t slot = (h >> 2) & (BHG_SE_DCNT - 1u), sh8 = 8 * (h & 3);
-    atomicAdd(&dcnt[slot], valid ? 1u << sh8 : 0u);  // unconditional: no exec-mask branch
+    const uint32_t one = valid ? 1u << sh8 : 0u;
+    atomicAdd(&dcnt[slot], one);  // unconditional: no exec-mask branch
     wsync();
-    const bool maybe_dup = valid && ((dcnt[slot] >> sh8) & 0xffu) > 1;
-    const uint64_t dm0 = __ballot(maybe_dup);
+    const uint32_t cnt = dcnt[slot];
+    wsync();
+    atomicSub(&dcnt[slot], one);
+    const uint64_t dm0 = __ballot(valid && ((cnt >> sh8) & 0xffu) > 1);
 #ifdef BHG_SE_PROF
     acc[6] += 1;
     acc[7] += __builtin_popcountll(dm0);
 #endif
+    // in increasing lane order i: lanes above i with i's hash take pos_i as candidate (the
+    // last such i wins), and lane i notes the first lane above it with its hash (nxt: it
+    // stores into the table only if no later updating lane shares its bucket)
+    const uint32_t c0 = c;
+    uint32_t nxt = 64;
     uint64_t dm = dm0;
-    bool chg = false;
     while (dm) {
-        const uint32_t i = __builtin_ctzll(dm);
+        const uint32_t i = (uint32_t)__builtin_ctzll(dm);
         dm &= dm - 1;
         const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
-        if (valid && lane > i && hi == h) {   // lanes visited in increasing i: last wins
-            c = pi;
-            chg = true;
-        }
+        const uint64_t above = __ballot(h == hi) & (~1ull << i);   // lanes > i with hash hi
+        if ((above >> lane) & 1) c = pi;
+        if (lane == i) nxt = above ? (uint32_t)__builtin_ctzll(above) : 64u;
     }
-    atomicSub(&dcnt[slot], valid ? 1u << sh8 : 0u);
-    wsync();
-    if (__ballot(chg)) eq = ld32a(in32, c) == u;
-    m = valid && eq;
+    if (__ballot(c != c0)) eq = ld32a(in32, c) == u;
+    const bool m = valid && eq;
     const uint64_t ev = __ballot(lane < nl && (!valid || m));
     const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
-    // table updates: iterations before the event, plus the event itself when it is a match;
-    // of the updating lanes with one bucket only the last one stores (plain u16 store)
-    const bool upd = valid && (lane < js || (lane == js && m));
-    bool last = upd;
-    dm = dm0 & __ballot(upd);
-    while (dm) {
-        const uint32_t i = __builtin_ctzll(dm);
-        dm &= dm - 1;
-        if (lane_val(h, i) == h && i > lane) last = false;
-    }
-    if (last) tab[h] = (se_tab_t)pos;
+    m_js = js < 64 && lane_val((uint32_t)m, js) != 0;
+    // updating iterations: the lanes before the event, and the event itself when it is a match
+    uint32_t nu = js + (m_js ? 1u : 0u);
+    if (nu > nl) nu = nl;
+    if (lane < nu && nxt >= nu) tab[h] = (se_tab_t)pos;
     wsync();
     return js;
 }
@@ -311,7 +310,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint32_t js = se_batch(in32, tab, dcnt, lane, 33, valid, pos, u, h, c, eq, m, acc);
             if (js < 33) {
                 found = true;
-                if (lane_val((uint32_t)m, js) == 0) remainder = true;
+                if (!m) remainder = true;
                 else { s = lane_val(pos, js); cand = lane_val(c, js); }
             }
             kb = 33;
@@ -335,7 +334,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint32_t js = se_batch(in32, tab, dcnt, lane, 64, valid, pos, u, h, c, eq, m, acc);
             if (js < 64) {
                 found = true;
-                if (lane_val((uint32_t)m, js) == 0) remainder = true;
+                if (!m) remainder = true;
                 else { s = lane_val(pos, js); cand = lane_val(c, js); }
             }
         }
@@ -528,7 +527,8 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                 for (uint32_t t = blen + lane; t < blen + 16; t += 64) in[t] = 0;
                 uint32_t ts = 256;
                 while (ts < 16384 && ts < blen) ts *= 2;
-                for (uint32_t t = lane; t < ts; t += 64) tab[t] = 0;
+                for (uint32_t t = 8 * lane; t < ts; t += 512)   // 16 B per lane per store (ts >= 256)
+                    *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
                 wsync();
                 se_block_lds(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
             } else {
@@ -573,6 +573,9 @@ hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32
 // workgroups only when the first ones finish
 uint32_t snappy_enc_grid(const Launch &L, uint32_t n) {
     static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc, 64, BHG_SE_WAVES);
+#ifdef BHG_SE_MAXW  // lab: fewer resident waves per CU, to see how the encoder scales with occupancy
+    if (per_cu > BHG_SE_MAXW) return (uint32_t)L.num_cus * BHG_SE_MAXW < n ? (uint32_t)L.num_cus * BHG_SE_MAXW : n;
+#endif
     uint32_t g = (uint32_t)L.num_cus * (uint32_t)per_cu;
     if (g > n) g = n;
     return g ? g : 1;
