@@ -190,12 +190,13 @@ __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, u
     r.n = 0;
 }
 
-__device__ __forceinline__ void se_push(Out &o, const uint8_t *in, OpRing &r, uint32_t lane, uint32_t base,
-                                        uint32_t lit, uint32_t cl, uint32_t off) {
+// op n of the ring (the caller flushes a full ring before the next push)
+__device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t base, uint32_t lit, uint32_t cl,
+                                        uint32_t off) {
     const bool mine = lane == r.n;  // v_cmp + two v_cndmask: no exec-mask branch
     r.a = mine ? base | lit << 16 : r.a;
     r.b = mine ? cl | off << 16 : r.b;
-    if (++r.n == 64) se_flush(o, in, r, lane);
+    r.n++;
 }
 
 // First mismatch r in [0, 256) of in[c + r] vs in[s + r] (256 if all equal), 4 bytes per lane
@@ -353,8 +354,6 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         // store between now and Go's lookup at the copy end e is tab[prevHash] = e - 1, and
         // prevHash == currHash is resolved by a compare.  So the lookup costs no LDS round
         // trip after the compare; copies ending at s + 64 or later take a serial lookup.
-        bool to_rem = false;
-        uint32_t lit = s - nextEmit;
         for (;;) {
             const uint32_t A = ld32a(in32, s + 4 * lane);
             const uint32_t B = ld32a(in32, cand + 4 * lane);
@@ -362,12 +361,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint32_t hU = se_hash(U, shift) & tmask;
             const uint32_t tU = tab[hU];
             uint32_t f = min(se_mismatch(A, B), len - s);
-            if (f < 4u) {  // the chained candidate does not match: back to scanning at s + 1
-                s += 1;
+            if (f < 4u) {  // the chained candidate does not match: scanning resumes at s + 1
                 Uw = U;
                 hUw = hU;
                 tUw = tU;
-                fast = true;
                 break;
             }
             uint32_t r0 = s;  // start of the round that found the mismatch
@@ -376,12 +373,11 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 f = min(se_mismatch(ld32a(in32, r0 + 4 * lane), ld32a(in32, cand + (r0 - s) + 4 * lane)), len - r0);
             }
             const uint32_t e = r0 + f;
-            se_push(o, in, r, lane, s, lit, e - s, s - cand);
-            lit = 0;
+            se_push(r, lane, s, s - nextEmit, e - s, s - cand);  // literal run only before the first copy
+            nextEmit = e;
             const uint32_t q = e - s;
             s = e;
-            nextEmit = s;
-            if (s >= sLimit) { to_rem = true; break; }
+            if (s >= sLimit) break;
             uint32_t prevHash, currHash, tc;
             if (q < 64u) {
                 prevHash = lane_val(hU, q - 1);
@@ -393,21 +389,27 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 currHash = se_hash(x0 >> 8 | x1 << 24, shift) & tmask;
                 tc = uni(tab[currHash]);
             }
+            // tab[prevHash] = s - 1, then tab[currHash] = s: one store by lanes 0 and 1 (when
+            // the slots coincide both lanes store s)
+            const bool same = prevHash == currHash;
             wsync();
-            if (lane == 0) {
-                tab[prevHash] = (se_tab_t)(s - 1);
-                tab[currHash] = (se_tab_t)s;
-            }
-            cand = prevHash == currHash ? s - 1 : tc;
+            if (lane < 2) tab[lane ? currHash : prevHash] = (se_tab_t)(lane || same ? s : s - 1);
+            cand = same ? s - 1 : tc;
             wsync();
+            if (r.n == 64) se_flush(o, in, r, lane);
         }
 #ifdef BHG_SE_PROF
         SE_T(t_cp1);
         acc[2] += t_cp1 - t_scan1;
 #endif
-        if (to_rem) break;
+        if (s >= sLimit) break;
+        s += 1;
+        fast = true;
     }
-    if (nextEmit < len) se_push(o, in, r, lane, len, len - nextEmit, 0, 0);
+    if (nextEmit < len) {
+        if (r.n == 64) se_flush(o, in, r, lane);
+        se_push(r, lane, len, len - nextEmit, 0, 0);
+    }
     if (r.n) se_flush(o, in, r, lane);
 }
 
