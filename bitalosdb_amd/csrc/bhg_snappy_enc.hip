@@ -19,9 +19,6 @@
 namespace bhg {
 
 typedef u32x4 u32x4u __attribute__((aligned(1)));
-#ifndef BHG_SE_U16
-#define BHG_SE_U16 1  // measured with the register skip offsets: 49.4 GiB/s (11 waves/CU) vs 37.7 (u32, 7)
-#endif
 #ifndef BHG_SE_STAGE16
 #define BHG_SE_STAGE16 1  // measured: C4 30.7 vs 30.0 GiB/s (u16 table: 28.1 at 7 waves, 26.5 at 12)
 #endif
@@ -31,17 +28,18 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_WAVES
 #define BHG_SE_WAVES 7
 #endif
-#if BHG_SE_U16
+// the hash table holds u16 positions (blocks here are <= 4 KiB): 13 KiB of LDS per wave,
+// 11 waves per CU (a u32 table: 7 waves per CU, 37.7 vs 49.4 GiB/s in round 2)
 typedef uint16_t se_tab_t;
-#else
-typedef uint32_t se_tab_t;
-#endif
 
 #define SE_CAP 4096                 // LDS block capacity
 #define SE_TAB 4096                 // LDS table entries (tableSize <= 4096 when len <= 4096)
 #define SE_MAXBLOCK 65536           // encode.go maxBlockSize
 #define SE_MARGIN 15                // inputMargin
 #define SE_MINNONLIT 17             // minNonLiteralBlockSize
+// table index of 64 scratch u16 slots after the table and the dedupe counters: lanes that
+// must not store write there instead of being masked off (no exec-mask branch)
+#define SE_DUMMY (SE_TAB + 2 * BHG_SE_DCNT)
 
 struct SkipTab {
     uint32_t f[1025];
@@ -124,23 +122,34 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
 // The matcher does not write output bytes.  Every copy it finds becomes one op --
-// (copy start, length of the literal run before it, copy length, offset), the block's
-// final literal an op with copy length 0 -- written into lane n of two VGPRs by a
-// select (no exec-mask branch, nothing on the dependency chain).  Every 64 ops
+// (copy start, copy end, candidate: the literal run before it ends where the previous op
+// ended), the block's final literal an op with copy length 0 -- written into lane n of
+// three VGPRs by selects.  Every 64 ops
 // se_flush turns them into golang/snappy's bytes with all lanes at once: per-op sizes
 // (emitLiteral header + literal + emitCopy tags), a wave prefix sum for the output
 // offsets, tags written by their own lanes, literal bytes copied from the LDS block by
 // the whole wave.
 struct OpRing {
-    uint32_t a;  // lane k: op k's copy start | literal length << 16
-    uint32_t b;  // lane k: op k's copy length | offset << 16
-    uint32_t n;  // ops held (wave-uniform)
+    uint32_t s;   // lane k: op k's copy start (the final literal: the block length)
+    uint32_t e;   // lane k: op k's copy end (its literal run is [end of op k - 1, s))
+    uint32_t c;   // lane k: op k's candidate (offset s - c)
+    uint32_t n;   // ops held (wave-uniform)
+    uint32_t e0;  // end of the op before lane 0's (wave-uniform)
 };
+
+// lane i <- lane i - 1 (DPP wave_shr:1, bound_ctrl off: lane 0, whose source is out of
+// range, keeps `first`)
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
+}
 
 __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, uint32_t lane) {
     const bool act = lane < r.n;
-    const uint32_t a = act ? r.a : 0u, b = act ? r.b : 0u;
-    const uint32_t base = a & 0xffffu, lit = a >> 16, cl = b & 0xffffu, off = b >> 16;
+    // (no lane-0 select here: the compiler turned one into an exec-masked branch around the
+    // DPP, and a DPP move reading an inactive lane returns `old`)
+    const uint32_t prev_e = lane_prev(r.e, r.e0);
+    const uint32_t base = r.s;
+    const uint32_t lit = act ? base - prev_e : 0u, cl = act ? r.e - base : 0u, off = base - r.c;
     const uint32_t lh = lit == 0 ? 0u : lit <= 60 ? 1u : lit <= 256 ? 2u : 3u;  // emitLiteral: n = lit - 1
     uint32_t L = cl, n64 = 0;
     if (L >= 68) {  // emitCopy: "for length >= 68 { 64-byte copy; length -= 64 }"
@@ -187,15 +196,17 @@ __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, u
         for (uint32_t t = lane; t < ll; t += 64) d0[t] = in[s0 + t];
     }
     o.d += total;
+    r.e0 = lane_val(r.e, r.n - 1);
     r.n = 0;
 }
 
-// op n of the ring (the caller flushes a full ring before the next push)
-__device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t base, uint32_t lit, uint32_t cl,
-                                        uint32_t off) {
-    const bool mine = lane == r.n;  // v_cmp + two v_cndmask: no exec-mask branch
-    r.a = mine ? base | lit << 16 : r.a;
-    r.b = mine ? cl | off << 16 : r.b;
+// op n of the ring (the caller flushes a full ring before the next push): three selects,
+// no exec-mask branch, nothing on the matcher's dependency chain
+__device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t s, uint32_t e, uint32_t c) {
+    const bool mine = lane == r.n;
+    r.s = mine ? s : r.s;
+    r.e = mine ? e : r.e;
+    r.c = mine ? c : r.c;
     r.n++;
 }
 
@@ -269,7 +280,7 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
     // updating iterations: the lanes before the event, and the event itself when it is a match
     uint32_t nu = js + (m_js ? 1u : 0u);
     if (nu > nl) nu = nl;
-    if (lane < nu && nxt >= nu) tab[h] = (se_tab_t)pos;
+    tab[lane < nu && nxt >= nu ? h : SE_DUMMY + lane] = (se_tab_t)pos;   // others: a scratch slot each
     wsync();
     return js;
 }
@@ -285,9 +296,11 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
     const uint32_t sLimit = len - SE_MARGIN;
     uint32_t nextEmit = 0, s = 1;
     OpRing r;
-    r.a = 0;
-    r.b = 0;
+    r.s = 0;
+    r.e = 0;
+    r.c = 0;
     r.n = 0;
+    r.e0 = 0;
     // after a copy chain ends, the copy loop's last (failed) check leaves in[s - 1 + lane ..)
     // (U), its hash (hU) and the table entry of that hash (tU) in this lane's registers
     bool fast = false;
@@ -373,7 +386,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 f = min(se_mismatch(ld32a(in32, r0 + 4 * lane), ld32a(in32, cand + (r0 - s) + 4 * lane)), len - r0);
             }
             const uint32_t e = r0 + f;
-            se_push(r, lane, s, s - nextEmit, e - s, s - cand);  // literal run only before the first copy
+            se_push(r, lane, s, e, cand);
             nextEmit = e;
             const uint32_t q = e - s;
             s = e;
@@ -393,7 +406,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // the slots coincide both lanes store s)
             const bool same = prevHash == currHash;
             wsync();
-            if (lane < 2) tab[lane ? currHash : prevHash] = (se_tab_t)(lane || same ? s : s - 1);
+            tab[lane == 0 ? prevHash : lane == 1 ? currHash : SE_DUMMY + lane] = (se_tab_t)(lane || same ? s : s - 1);
             cand = same ? s - 1 : tc;
             wsync();
             if (r.n == 64) se_flush(o, in, r, lane);
@@ -408,7 +421,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
     }
     if (nextEmit < len) {
         if (r.n == 64) se_flush(o, in, r, lane);
-        se_push(r, lane, len, len - nextEmit, 0, 0);
+        se_push(r, lane, len, len, len);
     }
     if (r.n) se_flush(o, in, r, lane);
 }
@@ -469,7 +482,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
     // one LDS buffer: block (+16 zero bytes), table, dedupe counters.  The aligned reads of
     // the copy loop reach up to 260 bytes past a position < SE_CAP: into the table, never past
     // the buffer, and masked by the block length.
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4 + BHG_SE_DCNT];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4 + BHG_SE_DCNT + 32];
     uint8_t *in = reinterpret_cast<uint8_t *>(lds);
     se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP + 16) / 4);
     uint32_t *dcnt = lds + (SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4;
