@@ -210,17 +210,6 @@ __device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t s, ui
     r.n++;
 }
 
-// First mismatch r in [0, 256) of in[c + r] vs in[s + r] (256 if all equal), 4 bytes per lane
-// from aligned reads; the caller clips it to the block end (min with len - s: bytes past len
-// are then never looked at, whatever they hold).
-__device__ __forceinline__ uint32_t se_mismatch(uint32_t A, uint32_t B) {
-    const uint32_t w = A ^ B;
-    const uint64_t mm = __ballot(w != 0);
-    if (!mm) return 256u;
-    const uint32_t k = (uint32_t)__builtin_ctzll(mm);
-    return 4 * k + ((uint32_t)__builtin_ctz(lane_val(w, k)) >> 3);
-}
-
 // lane i <- lane i + 1 (DPP wave_shl:1; lane 63 gets 0)
 __device__ __forceinline__ uint32_t lane_next(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
@@ -359,21 +348,21 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
 #endif
         if (remainder) break;
         // ---- copies (encode_other.go's inner loop).  Each iteration reads, at once,
-        // A = in[s + 4 lane ..), B = in[cand + 4 lane ..) -- their compare both verifies the
+        // U = in[s + lane .. + 4) and in[cand + lane] -- the byte compare both verifies the
         // 4-byte match (Go's load32 check; always true for the scan's match) and extends it
-        // (Go extends from s + 4 after a verified match: the same first mismatch) -- and
-        // U = in[s + lane .. + 4), whose hashes are the table slots of every position the copy
-        // can end at below s + 64.  The table is read for all of them right away: the only
+        // 64 bytes a round (Go extends from s + 4 after a verified match: the same first
+        // mismatch) -- and U's hashes are the table slots of every position the copy can end
+        // at below s + 64.  The table is read for all of them right away: the only
         // store between now and Go's lookup at the copy end e is tab[prevHash] = e - 1, and
         // prevHash == currHash is resolved by a compare.  So the lookup costs no LDS round
         // trip after the compare; copies ending at s + 64 or later take a serial lookup.
         for (;;) {
-            const uint32_t A = ld32a(in32, s + 4 * lane);
-            const uint32_t B = ld32a(in32, cand + 4 * lane);
             const uint32_t U = ld32a(in32, s + lane);
+            const uint32_t V = in[cand + lane];
             const uint32_t hU = se_hash(U, shift) & tmask;
             const uint32_t tU = tab[hU];
-            uint32_t f = min(se_mismatch(A, B), len - s);
+            const uint64_t mm = __ballot((U & 0xffu) != V);
+            uint32_t f = min(mm ? (uint32_t)__builtin_ctzll(mm) : 64u, len - s);
             if (f < 4u) {  // the chained candidate does not match: scanning resumes at s + 1
                 Uw = U;
                 hUw = hU;
@@ -381,9 +370,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 break;
             }
             uint32_t r0 = s;  // start of the round that found the mismatch
-            while (f == 256u) {
-                r0 += 256;
-                f = min(se_mismatch(ld32a(in32, r0 + 4 * lane), ld32a(in32, cand + (r0 - s) + 4 * lane)), len - r0);
+            while (f == 64u) {
+                r0 += 64;
+                const uint64_t m2 = __ballot(in[r0 + lane] != in[cand + (r0 - s) + lane]);
+                f = min(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u, len - r0);
             }
             const uint32_t e = r0 + f;
             se_push(r, lane, s, e, cand);
@@ -479,9 +469,9 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                                                    uint32_t n, uint8_t *__restrict__ scratch, uint64_t scap,
                                                    const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
                                                    uint16_t *__restrict__ gtables) {
-    // one LDS buffer: block (+16 zero bytes), table, dedupe counters.  The aligned reads of
-    // the copy loop reach up to 260 bytes past a position < SE_CAP: into the table, never past
-    // the buffer, and masked by the block length.
+    // one LDS buffer: block (+16 zero bytes), table, dedupe counters, scratch store slots.
+    // The copy loop's compares read up to 67 bytes past a position < SE_CAP: into the
+    // table, never past the buffer, and clipped to the block length.
     __shared__ __attribute__((aligned(16))) uint32_t lds[(SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4 + BHG_SE_DCNT + 32];
     uint8_t *in = reinterpret_cast<uint8_t *>(lds);
     se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP + 16) / 4);
