@@ -301,8 +301,12 @@ namespace {
 // kernels and copies of the others; slot reuse is ordered by its stream.
 constexpr uint64_t kChunkBytesDefault = 64ull << 20;
 
+// Handles out of offset order end the pipeline where they start: the chunk walk below checks the order
+// as it goes (no separate host pass over the batch), the chunks already issued complete, and the
+// function returns -100 with *done = the handles decoded; the caller decodes the rest another way.
 int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles, uint32_t n,
-                          const uint32_t *expected_crc, bhg_desc *out_desc) {
+                          const uint32_t *expected_crc, bhg_desc *out_desc, uint32_t *done) {
+    *done = 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     uint64_t kChunkBytes = kChunkBytesDefault;
     if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) kChunkBytes = strtoull(e, nullptr, 10);  // tests
@@ -320,12 +324,19 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     bhg::Launch L = launch_of(c, nullptr);
     uint32_t a = 0;
     int slot = 0;
+    uint64_t prev_off = 0;
+    bool unsorted = false;
     while (a < n) {
         // grow the chunk while its byte span stays within kChunkBytes
         uint64_t lo = UINT64_MAX, hi = 0;
         uint32_t b = a;
         while (b < n && b - a < max_chunk_n) {
             const bhg_handle &h = handles[b];
+            if (h.offset < prev_off) {
+                unsorted = true;
+                break;
+            }
+            prev_off = h.offset;
             const bool inb = h.length != 0 && h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
             if (inb) {
                 const uint64_t nlo = h.offset < lo ? h.offset : lo;
@@ -340,9 +351,12 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
         const uint32_t cn = b - a;
         if (lo == UINT64_MAX) lo = hi = 0;
         const uint64_t span = hi - lo;
-        if (span > kChunkBytes) {  // a single record larger than the ring slot: decode it alone, unpipelined
+        if (span > kChunkBytes || cn == 0) {
+            // a single record larger than the ring slot, or handles out of order from a on: the caller
+            // decodes [a, n) unpipelined
             for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
-            return -100;  // caller falls back to the whole-batch path
+            *done = a;
+            return -100;
         }
         uint8_t *base = reinterpret_cast<uint8_t *>(c->pbuf[slot]) + kHead;
         bhg_handle *dh = reinterpret_cast<bhg_handle *>(base + al(kChunkBytes + 64));
@@ -363,8 +377,14 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
         HIP_TRY(c, hipMemcpyAsync(out_desc + a, dd, (size_t)cn * sizeof(bhg_desc), hipMemcpyDeviceToHost, s));
         a = b;
         slot = (slot + 1) % bhg_ctx::kPipe;
+        if (unsorted) {
+            for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
+            *done = a;
+            return -100;
+        }
     }
     for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
+    *done = n;
     return BHG_OK;
 }
 
@@ -432,15 +452,17 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (int r = set_device(c)) return r;
     std::lock_guard<std::mutex> g(c->mu);
     if (codec == BHG_CODEC_NONE) {
-        // sorted handles: the chunked pipeline (49.7 GiB/s with src, handles and descriptors pinned,
-        // 44 pageable; scripts/lab/e2e_lab.py); otherwise a mapped src is decoded in place (40 GiB/s),
-        // which beats copying all of src before the kernel
-        bool sorted = true;
-        for (uint32_t i = 1; i < n && sorted; i++) sorted = handles[i].offset >= handles[i - 1].offset;
-        if (sorted) {
-            const int r = decode_host_pipelined(c, src, src_len, handles, n, expected_crc, out_desc);
-            if (r != -100) return r;
-        }
+        // handles in offset order: the chunked pipeline (49.7 GiB/s with src, handles and descriptors
+        // pinned, 44 pageable; scripts/lab/e2e_lab.py); from the first handle out of order on (or an
+        // oversized record), a mapped src is decoded in place (40 GiB/s), which beats copying all of
+        // src before the kernel, else the whole-batch path below
+        uint32_t done = 0;
+        const int r = decode_host_pipelined(c, src, src_len, handles, n, expected_crc, out_desc, &done);
+        if (r != -100) return r;
+        handles += done;
+        out_desc += done;
+        if (expected_crc) expected_crc += done;
+        n -= done;
         if (const void *dsrc = mapped_device_ptr(src))
             return decode_host_mapped(c, static_cast<const uint8_t *>(dsrc), src_len, handles, n, expected_crc,
                                       out_desc);
@@ -586,16 +608,17 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     if (n == 0) return encode_empty(c, o, L.stream);
     if (!keys || !key_off || !trailers || !vals || !val_off || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
     const size_t lens_b = ((size_t)n + 1) * 8, vlen_b = ((size_t)n + 1) * 8, scan_b = bhg::scan_scratch_bytes(n);
-    size_t snap_b = 0, soff_b = 0, gt_b = 0;
+    size_t snap_b = 0, soff_b = 0, gt_b = 0, cls_b = 0;
     if (codec == BHG_CODEC_SNAPPY) {
         // sum MaxEncodedLen = 32 n + V + sum(v_i / 6) <= 32 n + V + V / 6 (encode.go MaxEncodedLen)
         snap_b = (size_t)(32ull * n + vals_len + vals_len / 6 + 64);
         soff_b = ((size_t)n + 1) * 8;
         gt_b = (size_t)bhg::snappy_enc_grid(L, n) * 16384 * 2;
+        cls_b = bhg::snappy_enc_list_bytes(n);
     }
     Scratch sc;
-    const size_t al5 = 5 * 256;
-    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b + al5, sc)) return r;
+    const size_t al6 = 6 * 256;
+    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b + cls_b + al6, sc)) return r;
     bhg::EncodeLaunch E;
     memset(&E, 0, sizeof E);
     E.lens = reinterpret_cast<uint64_t *>(sc.take(lens_b));
@@ -605,9 +628,10 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
         uint8_t *snap = sc.take(snap_b);
         uint64_t *soff = reinterpret_cast<uint64_t *>(sc.take(soff_b));
         uint16_t *gt = reinterpret_cast<uint16_t *>(sc.take(gt_b));
+        uint32_t *cls = reinterpret_cast<uint32_t *>(sc.take(cls_b));
         HIP_TRY(c, bhg::launch_snappy_maxlen(L, val_off, n, soff));
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, soff, soff, n, E.scan_scratch));
-        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, snap_b, soff, vlen, gt));
+        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, snap_b, soff, vlen, gt, cls));
         E.vbase = snap; E.vpos = soff; E.vlen = vlen;
     } else {
         HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));

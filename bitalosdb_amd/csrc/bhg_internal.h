@@ -112,10 +112,10 @@ hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_
 // bhg_snappy_enc.hip
 hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *out);
 uint32_t snappy_enc_grid(const Launch &L, uint32_t n);
-// values whose MaxEncodedLen slot would end past scap get clen = ~0 (-> BHG_ST_NO_SPACE)
+size_t snappy_enc_list_bytes(uint32_t n);  // the value-class lists launch_snappy_enc needs
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
                              uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
-                             uint16_t *gtables);
+                             uint16_t *gtables, uint32_t *lists);
 
 // bhg_tail.hip: Writer.writeTable's tail for many tables (include/bithashgpu.h bhg_table_tail)
 struct TailLaunch {

@@ -32,14 +32,21 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 // 11 waves per CU (a u32 table: 7 waves per CU, 37.7 vs 49.4 GiB/s in round 2)
 typedef uint16_t se_tab_t;
 
-#define SE_CAP 4096                 // LDS block capacity
-#define SE_TAB 4096                 // LDS table entries (tableSize <= 4096 when len <= 4096)
+#define SE_CAP 4096                 // LDS block capacity of the large-value kernel
+#define SE_CAP_SMALL 2048           // ... of the small-value kernel (values <= 2 KiB)
 #define SE_MAXBLOCK 65536           // encode.go maxBlockSize
 #define SE_MARGIN 15                // inputMargin
 #define SE_MINNONLIT 17             // minNonLiteralBlockSize
-// table index of 64 scratch u16 slots after the table and the dedupe counters: lanes that
-// must not store write there instead of being masked off (no exec-mask branch)
-#define SE_DUMMY (SE_TAB + 2 * BHG_SE_DCNT)
+// LDS of a wave with block capacity CAP: the block (+16 zero bytes), the table (CAP u16
+// entries: tableSize <= len), the dedupe counters, and 64 scratch u16 slots (SE_DUMMY, after
+// the table and the counters): lanes that must not store write there instead of being masked
+// off (no exec-mask branch)
+template <int CAP>
+struct SeLayout {
+    static constexpr uint32_t kTab = CAP;
+    static constexpr uint32_t kDummy = kTab + 2 * BHG_SE_DCNT;
+    static constexpr uint32_t kWords = (CAP + 16) / 4 + kTab * sizeof(se_tab_t) / 4 + BHG_SE_DCNT + 32;
+};
 
 struct SkipTab {
     uint32_t f[1025];
@@ -230,6 +237,7 @@ __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, c
 // iterations up to it.  `eq` holds in[c .. c + 4) == u for the pre-batch c; lanes whose
 // candidate changes are re-checked.  Returns the event lane (>= nl: none in this batch) and
 // m_js, whether it is a match.
+template <uint32_t DUMMY>
 __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                                              uint32_t nl, bool valid, uint32_t pos, uint32_t u, uint32_t h,
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
@@ -269,13 +277,14 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
     // updating iterations: the lanes before the event, and the event itself when it is a match
     uint32_t nu = js + (m_js ? 1u : 0u);
     if (nu > nl) nu = nl;
-    tab[lane < nu && nxt >= nu ? h : SE_DUMMY + lane] = (se_tab_t)pos;   // others: a scratch slot each
+    tab[lane < nu && nxt >= nu ? h : DUMMY + lane] = (se_tab_t)pos;   // others: a scratch slot each
     wsync();
     return js;
 }
 
-// encodeBlock on an LDS-staged block (len in [17, SE_CAP]); tab zeroed by the caller.
+// encodeBlock on an LDS-staged block (len in [17, CAP]); tab zeroed by the caller.
 // f0 / f0n: this lane's skip offsets F[lane] and F[lane + 1] (the block's first batch).
+template <uint32_t DUMMY>
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                              uint32_t f0, uint32_t f0n, uint64_t *acc) {
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
@@ -310,7 +319,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const uint32_t pos = s + lane;
             const bool eq = ld32a(in32, valid ? c : 0u) == u;
             bool m;
-            const uint32_t js = se_batch(in32, tab, dcnt, lane, 33, valid, pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 33, valid, pos, u, h, c, eq, m, acc);
             if (js < 33) {
                 found = true;
                 if (!m) remainder = true;
@@ -334,7 +343,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
             const bool eq = ld32a(in32, c) == u;
             bool m;
-            const uint32_t js = se_batch(in32, tab, dcnt, lane, 64, valid, pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 64, valid, pos, u, h, c, eq, m, acc);
             if (js < 64) {
                 found = true;
                 if (!m) remainder = true;
@@ -396,7 +405,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // the slots coincide both lanes store s)
             const bool same = prevHash == currHash;
             wsync();
-            tab[lane == 0 ? prevHash : lane == 1 ? currHash : SE_DUMMY + lane] = (se_tab_t)(lane || same ? s : s - 1);
+            tab[lane == 0 ? prevHash : lane == 1 ? currHash : DUMMY + lane] = (se_tab_t)(lane || same ? s : s - 1);
             cand = same ? s - 1 : tc;
             wsync();
             if (r.n == 64) se_flush(o, in, r, lane);
@@ -464,18 +473,24 @@ rem:
     if (nextEmit < (int)len) se_emit_literal(o, nullptr, src + nextEmit, len - nextEmit, 0, 1);
 }
 
-// one wave per value: val bytes vals[val_off[i] .. val_off[i+1]) -> scratch[soff[i] ..), clen[i]
+// one wave per value: val bytes vals[val_off[i] .. val_off[i+1]) -> scratch[soff[i] ..), clen[i],
+// for the values i = list[0 .. *cnt).  CAP: the LDS block capacity (SE_CAP_SMALL: the values
+// <= 2 KiB, whose 7.3 KiB of LDS lets VGPRs bound the waves per CU; SE_CAP: the others,
+// 13.2 KiB; blocks longer than CAP take the lane-0 path with its table in gtables).
+template <int CAP>
 __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
-                                                   uint32_t n, uint8_t *__restrict__ scratch, uint64_t scap,
+                                                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt,
+                                                   uint8_t *__restrict__ scratch, uint64_t scap,
                                                    const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
                                                    uint16_t *__restrict__ gtables) {
     // one LDS buffer: block (+16 zero bytes), table, dedupe counters, scratch store slots.
-    // The copy loop's compares read up to 67 bytes past a position < SE_CAP: into the
+    // The copy loop's compares read up to 67 bytes past a position < CAP: into the
     // table, never past the buffer, and clipped to the block length.
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4 + BHG_SE_DCNT + 32];
+    typedef SeLayout<CAP> LY;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LY::kWords];
     uint8_t *in = reinterpret_cast<uint8_t *>(lds);
-    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP + 16) / 4);
-    uint32_t *dcnt = lds + (SE_CAP + 16) / 4 + SE_TAB * sizeof(se_tab_t) / 4;
+    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (CAP + 16) / 4);
+    uint32_t *dcnt = lds + (CAP + 16) / 4 + LY::kTab * sizeof(se_tab_t) / 4;
     const uint32_t lane = threadIdx.x;
     for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
@@ -484,7 +499,9 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
 #ifdef BHG_SE_PROF
     const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
 #endif
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t n = *cnt;
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+        const uint32_t i = list[j];
         const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
         if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
             if (lane == 0) clen[i] = ~0ull;
@@ -511,7 +528,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
             const uint8_t *bs = src + b0;
             if (blen < SE_MINNONLIT) {
                 se_emit_literal(o, nullptr, bs, blen, lane);
-            } else if (blen <= SE_CAP) {
+            } else if (blen <= (uint32_t)CAP) {
 #if BHG_SE_STAGE16
                 // one 16-B load per lane per 1 KiB (one memory round trip), then the 16 zero bytes
                 for (uint32_t t = 16 * lane; t < blen; t += 1024) {
@@ -535,7 +552,7 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
                 for (uint32_t t = 8 * lane; t < ts; t += 512)   // 16 B per lane per store (ts >= 256)
                     *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
                 wsync();
-                se_block_lds(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
+                se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
             } else {
                 uint32_t d = o.d;
                 if (lane == 0) {
@@ -573,24 +590,63 @@ hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32
     return hipGetLastError();
 }
 
-// one wave per resident workgroup slot (LDS: 13 KiB per wave with the u16 table, 21 KiB
-// with u32 -- 11 / 7 per CU on MI355X): a grid past what is resident would start its extra
-// workgroups only when the first ones finish
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n) {
-    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc, 64, BHG_SE_WAVES);
+// values <= SE_CAP_SMALL -> list[0 ..), the others -> list[n ..); counts in cnt[0], cnt[1]
+// (zeroed by the caller).  Order within a list is the atomics' (it only schedules waves).
+__global__ __launch_bounds__(256) void k_enc_class(const uint64_t *__restrict__ val_off, uint32_t n,
+                                                   uint32_t *__restrict__ list, uint32_t *__restrict__ cnt) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < n; b += stride) {
+        const uint32_t i = b + lane;
+        const bool v = i < n;
+        const bool big = v && val_off[i + 1] - val_off[i] > SE_CAP_SMALL;
+        const uint64_t mb = __ballot(big), ms = __ballot(v && !big);
+        const uint64_t below = (1ull << lane) - 1;
+        uint32_t bs = 0, bb = 0;
+        if (lane == 0) {
+            bs = ms ? atomicAdd(&cnt[0], (uint32_t)__builtin_popcountll(ms)) : 0u;
+            bb = mb ? atomicAdd(&cnt[1], (uint32_t)__builtin_popcountll(mb)) : 0u;
+        }
+        bs = uni(bs);
+        bb = uni(bb);
+        if (v) {
+            if (big) list[n + bb + __builtin_popcountll(mb & below)] = i;
+            else list[bs + __builtin_popcountll(ms & below)] = i;
+        }
+    }
+}
+
+// one wave per resident workgroup slot (LDS-bound: 13.2 KiB per wave at SE_CAP -> 11 per CU
+// with 2-KiB allocation granules; 7.3 KiB at SE_CAP_SMALL -> VGPR-bound): a grid past what is
+// resident would start its extra workgroups only when the first ones finish
+template <int CAP>
+static uint32_t enc_grid(const Launch &L, uint32_t n) {
+    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP>, 64, BHG_SE_WAVES);
+    uint32_t pc = per_cu;
 #ifdef BHG_SE_MAXW  // lab: fewer resident waves per CU, to see how the encoder scales with occupancy
-    if (per_cu > BHG_SE_MAXW) return (uint32_t)L.num_cus * BHG_SE_MAXW < n ? (uint32_t)L.num_cus * BHG_SE_MAXW : n;
+    if (pc > BHG_SE_MAXW) pc = BHG_SE_MAXW;
 #endif
-    uint32_t g = (uint32_t)L.num_cus * (uint32_t)per_cu;
+    uint32_t g = (uint32_t)L.num_cus * pc;
     if (g > n) g = n;
     return g ? g : 1;
 }
 
+uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP>(L, n); }
+
+size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + 2) * 4; }
+
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
                              uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
-                             uint16_t *gtables) {
-    hipLaunchKernelGGL(k_snappy_enc, dim3(snappy_enc_grid(L, n)), dim3(64), 0, L.stream, vals, val_off, n, scratch,
-                       scap, soff, clen, gtables);
+                             uint16_t *gtables, uint32_t *lists) {
+    uint32_t *cnt = lists + 2 * (size_t)n;
+    if (hipError_t e = hipMemsetAsync(cnt, 0, 8, L.stream)) return e;
+    hipLaunchKernelGGL(k_enc_class, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, val_off, n, lists, cnt);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(k_snappy_enc<SE_CAP_SMALL>, dim3(enc_grid<SE_CAP_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
+                       val_off, (const uint32_t *)lists, (const uint32_t *)cnt, scratch, scap, soff, clen, gtables);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(k_snappy_enc<SE_CAP>, dim3(enc_grid<SE_CAP>(L, n)), dim3(64), 0, L.stream, vals, val_off,
+                       (const uint32_t *)lists + n, (const uint32_t *)cnt + 1, scratch, scap, soff, clen, gtables);
     return hipGetLastError();
 }
 

@@ -621,3 +621,37 @@ def test_host_mapped_unsorted(codec, pin_desc):
     exp, _, _ = O.decode_batch(src, h, expected_crc=expected)
     assert_desc_equal(got, exp)
     assert (got["status"] == O.CRC_MISMATCH).sum() > 0
+
+
+@pytest.mark.parametrize("pin", [False, True])
+def test_host_pipelined_then_unsorted(pin, monkeypatch):
+    """bhg_decode_batch_host with handles in offset order up to an index and out of
+    order after it: the pipeline decodes the ordered prefix (several chunks), the rest
+    goes to the mapped (pinned src) or whole-batch (pageable) path; every descriptor
+    equals the restatement's."""
+    from bitalosdb_amd.codec import BithashCodec
+    monkeypatch.setenv("BHG_HOST_CHUNK_BYTES", str(1 << 16))
+    c = BithashCodec(0)
+    rng = random.Random(123)
+    specs = [(rand_bytes(rng, 32), rand_bytes(rng, rng.choice([64, 1024, 2000])), 5) for _ in range(3000)]
+    src, h = make_records(rng, specs, gap_max=3)
+    h = h.copy()
+    cut = 1700
+    tail = h[cut:].copy()
+    h[cut:] = tail[np.random.default_rng(8).permutation(len(tail))]
+    h["length"][50] = 0                        # ErrBhIllegalBlockLength inside the ordered prefix
+    exp0, _, _ = O.decode_batch(src, h)
+    expected = exp0["crc"].copy()
+    expected[7::61] ^= 1
+    buf = np.frombuffer(src, np.uint8).copy()
+    if pin:
+        c.host_register(buf)
+    try:
+        got, _, _ = c.decode_host(buf, h, expected_crc=expected)
+    finally:
+        if pin:
+            c.host_unregister(buf)
+    exp, _, _ = O.decode_batch(src, h, expected_crc=expected)
+    assert_desc_equal(got, exp)
+    assert (got["status"] == O.CRC_MISMATCH).sum() > 0
+    c.close()
