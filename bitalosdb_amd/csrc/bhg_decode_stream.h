@@ -125,14 +125,18 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
     const uint32_t tstride = gridDim.x * WPB;
     // wave-major tile index: waves that take one tile more than the others are spread over every CU
     uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    bhg_handle hn = {0, 0, 0};
-    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    // the next tile's handles and the expected CRCs are loaded with no branch around them
+    // (index clamped; see fetch below for why)
+    auto hidx = [&](uint32_t t) { const uint32_t x = t * 64 + lane; return x < n ? x : n - 1; };
+    const uint32_t *ecp = expected_crc != nullptr ? expected_crc : gtab;
+    const uint32_t emask = expected_crc != nullptr ? 0xffffffffu : 0u;
+    bhg_handle hn = handles[hidx(tile < ntiles ? tile : 0)];
     for (; tile < ntiles; tile += tstride) {
         const bhg_handle h = hn;
         const uint32_t i = tile * 64 + lane;
         {
             const uint32_t tn = tile + tstride;
-            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
+            hn = handles[hidx(tn < ntiles ? tn : tile)];
         }
         const bool valid = i < n;
         uint32_t st = BHG_ST_OK;
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         const uint64_t p = base + (inb ? h.offset : 0ull);
         const uint32_t m = (uint32_t)(((uint64_t)L + WIN - 1) / WIN);
         const uint32_t pad = (uint32_t)WIN * m - L;  // 0..WIN-1 (head left padding)
-        const uint32_t ecrc = (expected_crc != nullptr && valid) ? expected_crc[i] : 0u;
+        const uint32_t ecrc = ecp[(i < n ? i : n - 1) & emask];
         // record-major window numbering: M = exclusive prefix of m over the tile
         const uint32_t incl = wave_incl_add(m);
         const uint32_t M = incl - m;
@@ -434,13 +438,25 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                     if (MODE == 0) {
                         dvo = 12 + k; dvl = v;  // noCompressor.Decode: zero-copy view (compress.go:57-59)
                     } else {
-                        // snappy decodedLen (golang/snappy decode.go decodedLen); the value is decoded later
+                        // snappy decodedLen (golang/snappy decode.go decodedLen); the value is decoded later.
+                        // Its bytes come from the header words when they lie in the first 60 B (k <= 43:
+                        // a varint of <= 5 bytes), else from memory.
                         uint64_t x = 0;
                         uint32_t s = 0, hdr = 0;
                         bool ok = false;
                         const uint64_t vp = p + 12 + k;
+                        const bool inw = k <= 43;
                         for (uint32_t b = 0; b < 10 && b < v; b++) {
-                            const uint32_t c = gld<uint8_t>(vp + b);
+                            uint32_t c;
+                            if (inw && b < 5) {
+                                const uint32_t o = 12 + k + b;  // < 60
+                                uint32_t wd = 0;
+#pragma unroll
+                                for (uint32_t u = 0; u < 15; u++) wd = (o >> 2) == u ? rw[u] : wd;
+                                c = (wd >> (8 * (o & 3))) & 0xffu;
+                            } else {
+                                c = gld<uint8_t>(vp + b);
+                            }
                             if (c < 0x80) {
                                 ok = !(b == 9 && c > 1);
                                 x |= (uint64_t)c << s;

@@ -139,6 +139,11 @@ hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64
 // bhg_scan.hip: exclusive prefix sum of n u64 in place into out[0..n], out[n] = total.
 // scratch must hold scan_scratch_bytes(n).
 size_t scan_scratch_bytes(uint64_t n);
+// bhg_sort.hip: stable LSD radix sort of (u64 key, u32 value) pairs over key bits [0, end_bit);
+// the sorted pairs land in keys_out / vals_out, keys / vals are overwritten
+size_t radix_sort_scratch_bytes(uint32_t n);
+hipError_t launch_radix_sort_pairs(const Launch &L, uint64_t *keys, uint64_t *keys_out, uint32_t *vals,
+                                   uint32_t *vals_out, uint32_t n, uint32_t end_bit, void *scratch);
 hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch);
 
 // bhg_tscan.hip: table data-region scan (count -> scan -> write); first[ntables+1],

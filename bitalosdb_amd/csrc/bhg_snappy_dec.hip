@@ -281,30 +281,44 @@ __device__ __forceinline__ uint32_t sl_pos(uint32_t clen) {
     return ((uint32_t)SLOT - 8u - ((clen + 15u) & ~15u)) & ~15u;
 }
 
-// All loads first and unconditional (index clamped to n - 1), so the caller can
-// issue them ahead of the stream prefetch and wait for them alone (vmcnt is in
-// order: a wait for a load issued after the prefetch would wait for it too).
-template <int SLOT>
-__device__ __forceinline__ SlInfo sl_info(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
-                                          const uint64_t *val_off, uint64_t base, uint64_t out_cap) {
+// A block's descriptor fields, loaded a group before they are used: sl_load issues the loads
+// (unconditional, index clamped to n - 1) and nothing reads the values until sl_finish, a
+// whole group later -- computing the mode right after the loads made the compiler wait for
+// them on the spot (a memory round trip per group).
+struct SlRaw {
+    uint64_t hoff, o0, o1;
+    uint32_t hlen, st, cpos, dlen, i;
+};
+__device__ __forceinline__ SlRaw sl_load(uint32_t i, uint32_t n, const bhg_desc *out, const bhg_handle *handles,
+                                         const uint64_t *val_off) {
     const uint32_t ii = i < n ? i : n - 1;
     const uint32_t *dw = reinterpret_cast<const uint32_t *>(out + ii);
-    const uint32_t st = dw[9];
-    const uint32_t cpos = dw[2], dlen = dw[3];  // provisional (header pass): value position in the record, decoded length
+    SlRaw r;
+    r.st = dw[9];
+    r.cpos = dw[2];  // provisional (header pass): value position in the record
+    r.dlen = dw[3];  // ... decoded length
     const bhg_handle h = handles[ii];
-    const uint64_t o0 = val_off[ii], o1 = val_off[ii + 1];
+    r.hoff = h.offset;
+    r.hlen = h.length;
+    r.o0 = val_off[ii];
+    r.o1 = val_off[ii + 1];
+    r.i = i;
+    return r;
+}
+template <int SLOT>
+__device__ __forceinline__ SlInfo sl_finish(const SlRaw &w, uint32_t n, uint64_t base, uint64_t out_cap) {
     SlInfo r;
-    r.cp = base + h.offset + cpos;
-    r.o0 = o0;
-    r.clen = h.length - cpos;
-    r.dlen = dlen;
-    r.status = st;
-    if (i >= n || (st != BHG_ST_OK && st != BHG_ST_CRC_MISMATCH))
+    r.cp = base + w.hoff + w.cpos;
+    r.o0 = w.o0;
+    r.clen = w.hlen - w.cpos;
+    r.dlen = w.dlen;
+    r.status = w.st;
+    if (w.i >= n || (w.st != BHG_ST_OK && w.st != BHG_ST_CRC_MISMATCH))
         r.mode = SL_SKIP;
-    else if (o1 > out_cap || o1 - o0 < dlen)
+    else if (w.o1 > out_cap || w.o1 - w.o0 < w.dlen)
         r.mode = SL_TOOLARGE;
     else
-        r.mode = (dlen <= 1024u && r.clen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
+        r.mode = (w.dlen <= 1024u && r.clen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
     return r;
 }
 
@@ -321,6 +335,10 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
     // measured no faster)
     auto tag_at = [&](uint32_t p) -> uint64_t { return *reinterpret_cast<const u64_lds_u *>(lds + p); };
     uint64_t t8 = tag_at(s);
+    // lgkmcnt(0) here: the first tag is then complete on entry as on the back edge (where the
+    // next tag's read completes before the op's write), and the loop head needs no wait -- it
+    // used to wait there for the previous element's last write
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     while (s < se) {
         const uint32_t tag = (uint32_t)t8 & 0xffu, ty = tag & 3u, x = tag >> 2;
         const uint32_t b14 = (uint32_t)(t8 >> 8);  // the 4 bytes after the tag
@@ -357,8 +375,15 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
         const uint32_t big = mlit | (0u - (uint32_t)(off >= 16u));
         const uint32_t sstep = big & 16u;
         const uint32_t dstep = (big & 16u) | (~big & off);
-        for (uint32_t t = 0, r = 0; t < n; t += dstep, r += sstep)
+        // n >= 1 here (n == 0 is `bad`): a do-while, so the compiler sees that the next tag's read
+        // (issued before the first op's read, which the op waits for) is complete at the loop head
+        // and does not wait there for the last op's write as well
+        uint32_t t = 0, r = 0;
+        do {
             *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
+            t += dstep;
+            r += sstep;
+        } while (t < n);
         d += n;
         s = sn;
         t8 = t8n;
@@ -382,11 +407,11 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
-    auto info = [&](uint32_t grp) -> SlInfo {
+    auto load = [&](uint32_t grp) -> SlRaw {
         const uint32_t i = grp * BPW + lane;
-        SlInfo r = sl_info<SLOT>(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off, base, out_cap);
-        return r;
+        return sl_load(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off);
     };
+    auto info = [&](uint32_t grp) -> SlInfo { return sl_finish<SLOT>(load(grp), n, base, out_cap); };
     u32x4 v[BPW];
     // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
     // past the stream load src + 0; the dump drops them) and clamped to end
@@ -427,7 +452,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
         }
         sl_wsync();
         // 2. descriptors of the group after next, then the next group's streams in flight
-        const SlInfo nn = info(g + 2 * G);
+        const SlRaw nn = load(g + 2 * G);
         prefetch(nxt);
         // 3. decode
         uint32_t fin = cur.status, mode = cur.mode;
@@ -470,7 +495,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             dw[9] = fin;
         }
         cur = nxt;
-        nxt = nn;
+        nxt = sl_finish<SLOT>(nn, n, base, out_cap);
     }
 }
 

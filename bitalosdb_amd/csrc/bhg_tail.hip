@@ -16,7 +16,8 @@
 // test per run, last-occurrence flags, then every byte of the tail:
 //
 //   k_tail_keys    lane/record: sort key (table << 32 | khash), invalid -> ~0
-//   radix sort     rocprim, stable (add order kept inside a run)
+//   radix sort     bhg_sort.hip, stable (add order kept inside a run), key bits
+//                  [0, 32 + bits(ntables)): invalid keys (~0) stay above every valid one
 //   k_tail_heads   lane/position: run-head flags -> scan -> run index
 //   k_tail_runs    lane/run: run position, key, length, conflict flag
 //   k_tail_keep    lane/position: last occurrence of its key in a conflict run
@@ -35,8 +36,6 @@
 //   k_tail_crch    lane/table: HashIndex header, checksum range
 //   k_crc_long     the indexhash_data checksum (bhg_decode.hip)
 //   k_tail_finish  lane/table: block headers, checksum entry, meta block, footer
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -517,12 +516,13 @@ __global__ __launch_bounds__(64) void k_tail_finish(TailArgs a) {
     }
 }
 
-size_t sort_tmp_bytes(uint32_t n) {
-    size_t b = 0;
-    if (rocprim::radix_sort_pairs(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr, (const uint32_t *)nullptr,
-                                  (uint32_t *)nullptr, n, 0, 64, (hipStream_t)0) != hipSuccess)
-        return 0;
-    return b;
+size_t sort_tmp_bytes(uint32_t n) { return radix_sort_scratch_bytes(n); }
+
+// key bits the sort looks at: khash (32) + the table index; ntables itself fits too, so a
+// truncated invalid key (~0) is above every valid key
+uint32_t sort_end_bit(uint32_t ntables) {
+    const uint32_t tb = ntables ? 32u - (uint32_t)__builtin_clz(ntables) : 1u;
+    return 32u + tb > 64u ? 64u : 32u + tb;
 }
 
 }  // namespace
@@ -566,8 +566,7 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     e = hipMemsetAsync(a.cbound, 0, TT * 8, L.stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_keys, dim3(g), dim3(256), 0, L.stream, a);
-    e = rocprim::radix_sort_pairs(sort_buf, sort_tmp, (const uint64_t *)a.sk, a.sk_s, (const uint32_t *)a.idx, a.idx_s,
-                                  n, 0, 64, L.stream);
+    e = launch_radix_sort_pairs(L, a.sk, a.sk_s, a.idx, a.idx_s, n, sort_end_bit(nt), sort_buf);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_heads, dim3(g), dim3(256), 0, L.stream, a);
     if ((e = launch_exclusive_scan_u64(L, a.head, a.runidx, n, scan_s)) != hipSuccess) return e;

@@ -20,7 +20,7 @@ print('$tag', d['ms_per_step'], d['value'], r.get('kernel_avg_ms'), r.get('frac'
 for c in ${CONFIGS:-c2 c4}; do
   w=""; [ $c = c2 ] && w="--warmup 5"
   line ${c}_prod_t "" --config $c $w
-  for r in 1 2; do
+  for r in $(seq 1 ${ROUNDS:-2}); do
     for v in ${VARIANTS:-}; do line ${c}_${v}_$r $v --config $c $w --no-traffic; done
     line ${c}_prod_$r "" --config $c $w --no-traffic
   done

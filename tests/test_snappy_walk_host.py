@@ -32,6 +32,7 @@ def walk(tmp_path_factory):
     i1 = s.index("}  // namespace\n\ntemplate <int BPW")
     body = s[i0:i1].replace("__device__ __forceinline__ ", 'extern "C" ')
     hdr = ("#include <stdint.h>\n"
+           "#define __builtin_amdgcn_s_waitcnt(x) ((void)0)\n"   # a wait-count hint on the GPU
            "typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));\n"
            "typedef uint64_t u64_lds_u __attribute__((aligned(1), may_alias));\n"
            "typedef u32x4 u32x4_lds_u __attribute__((aligned(1), may_alias));\n")
