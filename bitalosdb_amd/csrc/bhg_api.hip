@@ -632,10 +632,10 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
         HIP_TRY(c, bhg::launch_snappy_maxlen(L, val_off, n, soff));
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, soff, soff, n, E.scan_scratch));
         HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, snap_b, soff, vlen, gt, cls));
-        E.vbase = snap; E.vpos = soff; E.vlen = vlen;
+        E.vbase = snap; E.vpos = soff; E.vlen = vlen; E.vend = snap + snap_b;
     } else {
         HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));
-        E.vbase = vals; E.vpos = val_off; E.vlen = vlen;
+        E.vbase = vals; E.vpos = val_off; E.vlen = vlen; E.vend = vals + vals_len;
     }
     E.keys = keys; E.key_off = key_off; E.trailers = trailers;
     E.n = n; E.file_nums = file_nums; E.max_tables = max_tables; E.init_size = init_size; E.table_max = table_max;
@@ -701,7 +701,7 @@ int bhg_repack_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     uint32_t *pre = reinterpret_cast<uint32_t *>(sc.take(N * 4));
     HIP_TRY(c, bhg::launch_repack_prep(L, src, src_len, handles, n, key_off, key_len, trailers, vpos, vlen, fns, pre));
     E.keys = src; E.key_off = key_off; E.key_len = key_len; E.trailers = trailers;
-    E.vbase = src; E.vpos = vpos; E.vlen = vlen; E.n = n;
+    E.vbase = src; E.vpos = vpos; E.vlen = vlen; E.vend = src + src_len; E.n = n;
     E.file_nums = fns; E.rec_file_nums = fns; E.live = live; E.khash = khash; E.pre_status = pre;
     E.single_table = 1; E.max_tables = 1; E.init_size = init_size; E.table_max = UINT64_MAX;
     E.out = out; E.out_cap = out_cap; E.o = *o;

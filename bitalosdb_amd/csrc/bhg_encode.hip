@@ -27,6 +27,7 @@ struct EncArgs {
     const uint64_t *key_off;
     const uint64_t *trailers;
     const uint8_t *vals;          // value' bytes base (raw values or snappy scratch)
+    uint64_t vals_end;            // end of the buffer vals points into (0: unknown; loads then stay in each value)
     const uint64_t *vpos;         // value' start offset per record (into vals)
     const uint64_t *vlen;         // value' length per record
     uint32_t n;
@@ -145,29 +146,34 @@ __device__ __forceinline__ uint32_t table_of(const uint32_t *ts, uint32_t nt, ui
 }
 
 #define ENC_WAVES 4
-#define ENC_PACK_K 6  // dwords per lane per record pass (1,536 B)
-// One WAVE per tile of 64 records.  Lane = record: the record's metadata (status, position,
-// sizes, key / value / trailer / fileNum) is loaded for the whole tile at once.  Then per
-// record (wave-uniform via readlane): the record's dwords q = d0 + 4 (lane + 64 k), k <
-// ENC_PACK_K, are assembled with every load issued before the first store -- value dwords from
-// two aligned loads and a byte funnel, the <= 56-B prefix (header | ukey | trailer) and the
-// record's partial first / last dwords byte by byte from registers and 8-B key / value windows.
-// (The wave-per-record version loaded the metadata record by record: ~6 dependent memory
-// round trips per record, 1.42 ms per C4 batch.)
+#define ENC_PACK_K 2  // 16-B value chunks per lane per record pass (2 KiB)
+// One WAVE per tile of 64 records (records are back to back in `out`).
+//  phase A, lane = record: metadata, then the record's prefix (header | ukey | trailer, <= 56 B
+//    for ukeys <= 36 B) and the value bytes up to the next 4-aligned output address qa,
+//    assembled byte by byte from registers (header, trailer) and dword windows of the key and
+//    the value head, and written as dwords (the first one, shared with the previous record, as
+//    bytes).  Per-byte work is spread over 64 records per instruction.
+//  phase B, wave per record: the value from qa on in 16-B output chunks (4-aligned dwordx4
+//    stores), each from a 20-B aligned source window and a byte funnel; two records per pass
+//    with all loads issued before the first store.
+// A record with a ukey > 36 B is packed byte by byte by its lane (rare; slow but exact).
+// (The wave-per-record version loaded the metadata record by record: ~6 dependent memory round
+// trips per record, 1.42 ms per C4 batch; the dword version of this one 1.05 ms.)
 __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = gridDim.x * ENC_WAVES;
     const uint32_t ntab = (uint32_t)a.o.summary[1];
     if (ntab == 0) return;  // split failed (max_tables too small)
     const uint32_t ntiles = (a.n + 63) / 64;
-    const uint64_t dummy = (uint64_t)a.lens;  // a valid address for loads whose result is unused
+    const uint64_t dummy = (uint64_t)a.lens;  // a valid, 16-B aligned address for loads whose result is unused
     for (uint32_t tile = blockIdx.x * ENC_WAVES + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
+        // ---------------- phase A: lane = record
         const uint32_t r = tile * 64 + lane;
         const uint32_t rr = r < a.n ? r : a.n - 1;
         const uint32_t st = a.o.status[rr];
         const uint64_t P = a.lens[rr];
         const uint32_t L = (uint32_t)(a.lens[rr + 1] - P);
-        const uint32_t klen = key_len_of(a, rr);
+        const uint32_t kl = key_len_of(a, rr);
         const uint32_t vl = (uint32_t)a.vlen[rr];
         const uint64_t kp = (uint64_t)a.keys + a.key_off[rr];
         const uint64_t tr = a.trailers[rr];
@@ -175,88 +181,137 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
         const uint32_t t = table_of(a.o.table_start, ntab, rr);
         const uint32_t fn = a.rec_file_nums != nullptr ? a.rec_file_nums[rr] : a.file_nums[t];
         const bool ok = r < a.n && st == BHG_ST_OK && fit_status(a, P, L) == BHG_ST_OK;
-        uint64_t todo = __ballot(ok);
+        const uint64_t dst = (uint64_t)a.out + P, dend = dst + L;
+        const uint32_t pre = 20 + kl;
+        const bool shortk = kl <= 36;
+        // output [q0, qa): the dwords holding the prefix (qa: first 4-aligned address >= the value start)
+        const uint64_t q0 = dst & ~3ull, vdst = dst + pre;
+        const uint64_t qa = (vdst + 3) & ~3ull;
+        const uint32_t sh = (uint32_t)(dst & 3);  // record offset of output byte q0 + x is x - sh
+        // key window: 10 dwords from ka (ukey <= 36 B at any alignment); value head: 2 dwords from va
+        uint32_t kw[10], vw[2];
+        const uint64_t ka = kp & ~3ull, va = vp & ~3ull, kend = kp + kl, vend = vp + vl;
+#pragma unroll
+        for (int u = 0; u < 10; u++) kw[u] = gld<uint32_t>(ok && shortk && ka + 4 * u < kend ? ka + 4 * u : dummy);
+#pragma unroll
+        for (int u = 0; u < 2; u++) vw[u] = gld<uint32_t>(ok && shortk && va + 4 * u < vend ? va + 4 * u : dummy);
+        if (ok && shortk) {
+            const uint32_t kd = (uint32_t)(kp - ka), vd = (uint32_t)(vp - va);
+            const uint32_t nq = (uint32_t)((qa - q0) >> 2);  // <= 16
+            for (uint32_t u = 0; u < nq; u++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    const int32_t o = (int32_t)(4 * u + b) - (int32_t)sh;  // record offset
+                    uint32_t by = 0;
+                    if (o >= 0 && o < 12) {
+                        const uint32_t hd = o < 4 ? kl + 8 : o < 8 ? vl : fn;
+                        by = (hd >> (8 * ((uint32_t)o & 3))) & 0xffu;
+                    } else if (o >= 12 && o < 12 + (int32_t)kl) {
+                        const uint32_t y = kd + (uint32_t)(o - 12);
+                        uint32_t wd = 0;
+#pragma unroll
+                        for (uint32_t z = 0; z < 10; z++) wd = (y >> 2) == z ? kw[z] : wd;
+                        by = (wd >> (8 * (y & 3))) & 0xffu;
+                    } else if (o >= 12 + (int32_t)kl && o < (int32_t)pre) {
+                        by = (uint32_t)(tr >> (8 * (uint32_t)(o - 12 - (int32_t)kl))) & 0xffu;
+                    } else if (o >= (int32_t)pre) {
+                        const uint32_t y = vd + (uint32_t)(o - (int32_t)pre);  // < 8
+                        by = ((y < 4 ? vw[0] : vw[1]) >> (8 * (y & 3))) & 0xffu;
+                    }
+                    x |= by << (8 * b);
+                }
+                const uint64_t q = q0 + 4ull * u;
+                if (q >= dst && q + 4 <= dend) {
+                    gst<uint32_t>(q, x);
+                } else {  // the first dword (shared with the previous record) or a record ending here
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++)
+                        if (q + b >= dst && q + b < dend) gst<uint8_t>(q + b, (uint8_t)(x >> (8 * b)));
+                }
+            }
+        } else if (ok) {  // ukey > 36 B: the whole record byte by byte
+            for (uint32_t o = 0; o < L; o++) {
+                uint32_t by;
+                if (o < 12) by = ((o < 4 ? kl + 8 : o < 8 ? vl : fn) >> (8 * (o & 3))) & 0xffu;
+                else if (o < 12 + kl) by = gld<uint8_t>(kp + (o - 12));
+                else if (o < pre) by = (uint32_t)(tr >> (8 * (o - 12 - kl))) & 0xffu;
+                else by = gld<uint8_t>(vp + (o - pre));
+                gst<uint8_t>(dst + o, (uint8_t)by);
+            }
+        }
+        // ---------------- phase B: wave per record, the value from qa on
+        uint64_t todo = __ballot(ok && shortk && qa < dend);
         while (todo) {
-            const int j = __builtin_ctzll(todo);
+            int jr[2];
+            jr[0] = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const uint64_t dst = (uint64_t)a.out + readlane_u64(P, j);
-            const uint32_t Lj = (uint32_t)__builtin_amdgcn_readlane((int)L, j);
-            const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)klen, j);
-            const uint32_t vlj = (uint32_t)__builtin_amdgcn_readlane((int)vl, j);
-            const uint32_t fnj = (uint32_t)__builtin_amdgcn_readlane((int)fn, j);
-            const uint64_t kpj = readlane_u64(kp, j), vpj = readlane_u64(vp, j), trj = readlane_u64(tr, j);
-            const uint32_t pre = 20 + kl;  // value starts at record offset pre
-            const uint64_t d0 = dst & ~3ull, vend = vpj + vlj, kend = kpj + kl;
-            const uint32_t nd = (uint32_t)((dst + Lj - d0 + 3) >> 2);  // dwords touched
-            for (uint32_t kb = 0; kb < nd; kb += 64 * ENC_PACK_K) {
-                // all loads first (addresses selected, never branched around), then the bytes
-                uint32_t v0[ENC_PACK_K], v1[ENC_PACK_K], k0[ENC_PACK_K], k1[ENC_PACK_K], w[ENC_PACK_K];
+            jr[1] = todo ? __builtin_ctzll(todo) : -1;
+            if (todo) todo &= todo - 1;
+            uint64_t qb[2], de[2], sb[2], ve[2];
+            uint32_t nc[2];
 #pragma unroll
-                for (int k = 0; k < ENC_PACK_K; k++) {
-                    const uint32_t idx = kb + lane + 64 * k;
-                    const int64_t o0 = (int64_t)(d0 + 4ull * idx - dst);  // record offset of the dword's first byte
-                    // value bytes (value offset o - pre) from the 8-B window at va
-                    const int64_t x0 = o0 - (int64_t)pre;
-                    const uint64_t va = (vpj + (uint64_t)(x0 > 0 ? x0 : 0)) & ~3ull;
-                    const bool vin = idx < nd && vlj != 0 && o0 + 3 >= (int64_t)pre && va < vend;
-                    v0[k] = gld<uint32_t>(vin ? va : dummy);
-                    v1[k] = gld<uint32_t>(vin && va + 4 < vend ? va + 4 : dummy);
-                    // key bytes (key offset o - 12) from the 8-B window at ka
-                    const int64_t y0 = o0 - 12;
-                    const uint64_t ka = (kpj + (uint64_t)(y0 > 0 ? y0 : 0)) & ~3ull;
-                    const bool kin = idx < nd && kl != 0 && o0 + 3 >= 12 && y0 < (int64_t)kl && ka < kend;
-                    k0[k] = gld<uint32_t>(kin ? ka : dummy);
-                    k1[k] = gld<uint32_t>(kin && ka + 4 < kend ? ka + 4 : dummy);
-                }
+            for (int h = 0; h < 2; h++) {
+                const int j = jr[h] < 0 ? jr[0] : jr[h];
+                qb[h] = readlane_u64(qa, j);
+                de[h] = readlane_u64(dend, j);
+                // source address of output byte qb: value offset qb - vdst
+                sb[h] = readlane_u64(vp, j) + (qb[h] - readlane_u64(vdst, j));
+                ve[h] = readlane_u64(vend, j);
+                nc[h] = jr[h] < 0 ? 0u : (uint32_t)((de[h] - qb[h] + 15) >> 4);
+            }
+            const uint32_t ncmax = nc[0] > nc[1] ? nc[0] : nc[1];
+            for (uint32_t cb = 0; cb < ncmax; cb += 64 * ENC_PACK_K) {
+                // loads: 20-B source windows (dwordx4 + dword) of both records' chunks
+                u32x4 wx[2][ENC_PACK_K];
+                uint32_t w4[2][ENC_PACK_K];
 #pragma unroll
-                for (int k = 0; k < ENC_PACK_K; k++) {
-                    const uint32_t idx = kb + lane + 64 * k;
-                    const int64_t o0 = (int64_t)(d0 + 4ull * idx - dst);
-                    const int64_t x0 = o0 - (int64_t)pre, y0 = o0 - 12;
-                    const uint64_t vs = vpj + (uint64_t)(x0 > 0 ? x0 : 0), va = vs & ~3ull;
-                    if (o0 >= (int64_t)pre) {  // whole dword in the value (or past the record end)
-                        w[k] = __builtin_amdgcn_alignbyte(v1[k], v0[k], (uint32_t)(vs & 3));
-                        continue;
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int k = 0; k < ENC_PACK_K; k++) {
+                        const uint32_t c = cb + lane + 64 * k;
+                        const uint64_t s = sb[h] + 16ull * c, sa = s & ~3ull;
+                        // a dword is loaded only if it holds a byte of the value, or lies inside the
+                        // buffer the value is in (vals_end)
+                        const uint64_t lim = a.vals_end > ve[h] ? a.vals_end : ((ve[h] + 3) & ~3ull);
+                        const bool use = c < nc[h];
+                        wx[h][k] = gld<u32x4_a4>(use && sa + 16 <= lim ? sa : dummy);
+                        w4[h][k] = gld<uint32_t>(use && sa + 20 <= lim ? sa + 16 : dummy);
                     }
-                    // prefix bytes: header (3 dwords) | key | trailer | value
-                    const uint64_t ka = (kpj + (uint64_t)(y0 > 0 ? y0 : 0)) & ~3ull;
-                    const uint64_t kw = (uint64_t)k0[k] | ((uint64_t)k1[k] << 32);
-                    const uint64_t vw = (uint64_t)v0[k] | ((uint64_t)v1[k] << 32);
-                    uint32_t x = 0;
 #pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        const int64_t o = o0 + b;
-                        uint32_t by = 0;
-                        if (o >= 0 && o < 12) {
-                            const uint32_t hd = o < 4 ? kl + 8 : o < 8 ? vlj : fnj;
-                            by = (hd >> (8 * ((uint32_t)o & 3))) & 0xffu;
-                        } else if (o >= 12 && o < 12 + (int64_t)kl) {
-                            by = (uint32_t)(kw >> (8 * (uint32_t)(kpj + (uint64_t)(o - 12) - ka))) & 0xffu;
-                        } else if (o >= 12 + (int64_t)kl && o < (int64_t)pre) {
-                            by = (uint32_t)(trj >> (8 * (uint32_t)(o - 12 - kl))) & 0xffu;
-                        } else if (o >= (int64_t)pre) {
-                            by = (uint32_t)(vw >> (8 * (uint32_t)(vpj + (uint64_t)(o - pre) - va))) & 0xffu;
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int k = 0; k < ENC_PACK_K; k++) {
+                        const uint32_t c = cb + lane + 64 * k;
+                        if (c >= nc[h]) continue;
+                        const uint64_t s = sb[h] + 16ull * c, sa = s & ~3ull;
+                        const uint64_t lim = a.vals_end > ve[h] ? a.vals_end : ((ve[h] + 3) & ~3ull);
+                        uint32_t d[5] = {wx[h][k].x, wx[h][k].y, wx[h][k].z, wx[h][k].w, w4[h][k]};
+                        if (sa + 20 > lim) {  // the value's last bytes at the end of its buffer: dword by dword
+#pragma unroll
+                            for (int z = 0; z < 5; z++) d[z] = sa + 4 * z < lim ? gld<uint32_t>(sa + 4 * z) : 0u;
                         }
-                        x |= by << (8 * b);
-                    }
-                    w[k] = x;
-                }
+                        const uint32_t f = (uint32_t)(s & 3);
+                        const u32x4 y = {__builtin_amdgcn_alignbyte(d[1], d[0], f), __builtin_amdgcn_alignbyte(d[2], d[1], f),
+                                         __builtin_amdgcn_alignbyte(d[3], d[2], f), __builtin_amdgcn_alignbyte(d[4], d[3], f)};
+                        const uint64_t q = qb[h] + 16ull * c;
+                        if (q + 16 <= de[h]) {
+                            gst<u32x4_a4>(q, y);
+                        } else {  // the record's last chunk: whole dwords, then the bytes of a partial one
+                            const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
-                for (int k = 0; k < ENC_PACK_K; k++) {
-                    const uint32_t idx = kb + lane + 64 * k;
-                    if (idx >= nd) continue;
-                    const uint64_t q = d0 + 4ull * idx;
-                    const int64_t o0 = (int64_t)(q - dst);
-                    if (o0 >= 0 && o0 + 4 <= (int64_t)Lj) {
-                        gst<uint32_t>(q, w[k]);
-                    } else {  // the record's partial first / last dword: neighbours own the other bytes
+                            for (int z = 0; z < 4; z++) {
+                                const uint64_t qz = q + 4 * z;
+                                if (qz + 4 <= de[h]) {
+                                    gst<uint32_t>(qz, yy[z]);
+                                } else {
 #pragma unroll
-                        for (int b = 0; b < 4; b++) {
-                            const int64_t o = o0 + b;
-                            if (o >= 0 && o < (int64_t)Lj) gst<uint8_t>(q + b, (uint8_t)(w[k] >> (8 * b)));
+                                    for (int b = 0; b < 4; b++)
+                                        if (qz + b < de[h]) gst<uint8_t>(qz + b, (uint8_t)(yy[z] >> (8 * b)));
+                                }
+                            }
                         }
                     }
-                }
             }
         }
     }
@@ -386,7 +441,7 @@ hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     EncArgs a;
     a.keys = E.keys; a.key_off = E.key_off; a.trailers = E.trailers;
-    a.vals = E.vbase; a.vpos = E.vpos; a.vlen = E.vlen;
+    a.vals = E.vbase; a.vpos = E.vpos; a.vlen = E.vlen; a.vals_end = (uint64_t)E.vend;
     a.n = E.n; a.file_nums = E.file_nums; a.rec_file_nums = E.rec_file_nums; a.live = E.live; a.khash = E.khash;
     a.key_len = E.key_len; a.pre_status = E.pre_status;
     a.single_table = E.single_table; a.max_tables = E.max_tables; a.init_size = E.init_size;

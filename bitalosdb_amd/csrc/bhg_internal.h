@@ -85,6 +85,7 @@ struct EncodeLaunch {
     const uint8_t *vbase;      // value' bytes (raw values or snappy scratch)
     const uint64_t *vpos;      // value' offsets into vbase
     const uint64_t *vlen;      // value' lengths
+    const uint8_t *vend;       // end of the buffer vbase points into (nullable: unknown)
     uint32_t n;
     const uint32_t *file_nums;      // per table
     const uint32_t *rec_file_nums;  // per record (AddIkey), nullable

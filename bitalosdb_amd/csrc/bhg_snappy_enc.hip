@@ -591,28 +591,49 @@ hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32
 }
 
 // values <= SE_CAP_SMALL -> list[0 ..), the others -> list[n ..); counts in cnt[0], cnt[1]
-// (zeroed by the caller).  Order within a list is the atomics' (it only schedules waves).
-__global__ __launch_bounds__(256) void k_enc_class(const uint64_t *__restrict__ val_off, uint32_t n,
-                                                   uint32_t *__restrict__ list, uint32_t *__restrict__ cnt) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < n; b += stride) {
-        const uint32_t i = b + lane;
+// (zeroed by the caller).  A workgroup of 16 waves takes 4,096 consecutive values and makes one
+// atomic per list (one per wave contended on two addresses: 0.36 ms per 1M values).  Order
+// within a list only schedules the encoder's waves.
+constexpr uint32_t kClassWaves = 16, kClassPer = 4;
+__global__ __launch_bounds__(64 * kClassWaves) void k_enc_class(const uint64_t *__restrict__ val_off, uint32_t n,
+                                                                uint32_t *__restrict__ list, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t wc[kClassWaves][2];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1;
+    const uint32_t b0 = blockIdx.x * (64 * kClassWaves * kClassPer);
+    uint64_t ms[kClassPer], mb[kClassPer];
+    uint32_t cs = 0, cb = 0;
+#pragma unroll
+    for (uint32_t it = 0; it < kClassPer; it++) {
+        const uint32_t i = b0 + it * 64 * kClassWaves + threadIdx.x;
         const bool v = i < n;
         const bool big = v && val_off[i + 1] - val_off[i] > SE_CAP_SMALL;
-        const uint64_t mb = __ballot(big), ms = __ballot(v && !big);
-        const uint64_t below = (1ull << lane) - 1;
-        uint32_t bs = 0, bb = 0;
-        if (lane == 0) {
-            bs = ms ? atomicAdd(&cnt[0], (uint32_t)__builtin_popcountll(ms)) : 0u;
-            bb = mb ? atomicAdd(&cnt[1], (uint32_t)__builtin_popcountll(mb)) : 0u;
+        mb[it] = __ballot(big);
+        ms[it] = __ballot(v && !big);
+        cs += (uint32_t)__builtin_popcountll(ms[it]);
+        cb += (uint32_t)__builtin_popcountll(mb[it]);
+    }
+    if (lane == 0) { wc[w][0] = cs; wc[w][1] = cb; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ts = 0, tb = 0;
+        for (uint32_t k = 0; k < kClassWaves; k++) {
+            const uint32_t s0 = wc[k][0], s1 = wc[k][1];
+            wc[k][0] = ts; wc[k][1] = tb;  // exclusive offsets of the waves
+            ts += s0; tb += s1;
         }
-        bs = uni(bs);
-        bb = uni(bb);
-        if (v) {
-            if (big) list[n + bb + __builtin_popcountll(mb & below)] = i;
-            else list[bs + __builtin_popcountll(ms & below)] = i;
-        }
+        const uint32_t bs = ts ? atomicAdd(&cnt[0], ts) : 0u, bb = tb ? atomicAdd(&cnt[1], tb) : 0u;
+        for (uint32_t k = 0; k < kClassWaves; k++) { wc[k][0] += bs; wc[k][1] += bb; }
+    }
+    __syncthreads();
+    uint32_t os = wc[w][0], ob = wc[w][1];
+#pragma unroll
+    for (uint32_t it = 0; it < kClassPer; it++) {
+        const uint32_t i = b0 + it * 64 * kClassWaves + threadIdx.x;
+        if ((mb[it] >> lane) & 1ull) list[n + ob + __builtin_popcountll(mb[it] & below)] = i;
+        if ((ms[it] >> lane) & 1ull) list[os + __builtin_popcountll(ms[it] & below)] = i;
+        os += (uint32_t)__builtin_popcountll(ms[it]);
+        ob += (uint32_t)__builtin_popcountll(mb[it]);
     }
 }
 
@@ -640,7 +661,9 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
                              uint16_t *gtables, uint32_t *lists) {
     uint32_t *cnt = lists + 2 * (size_t)n;
     if (hipError_t e = hipMemsetAsync(cnt, 0, 8, L.stream)) return e;
-    hipLaunchKernelGGL(k_enc_class, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, val_off, n, lists, cnt);
+    const uint32_t per = 64 * kClassWaves * kClassPer;
+    hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
+                       cnt);
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL(k_snappy_enc<SE_CAP_SMALL>, dim3(enc_grid<SE_CAP_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
                        val_off, (const uint32_t *)lists, (const uint32_t *)cnt, scratch, scap, soff, clen, gtables);
