@@ -25,6 +25,12 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_DCNT
 #define BHG_SE_DCNT 256  // dwords of byte counters for the in-batch duplicate check (4 buckets each)
 #endif
+#ifndef BHG_SE_QUEUE
+#define BHG_SE_QUEUE 1  // values handed to waves by a work queue (0: static round-robin, lab)
+#endif
+#ifndef BHG_SE_WPG
+#define BHG_SE_WPG 3    // waves per workgroup of the large-value launch
+#endif
 #ifndef BHG_SE_WAVES
 #define BHG_SE_WAVES 7
 #endif
@@ -474,12 +480,14 @@ rem:
 }
 
 // one wave per value: val bytes vals[val_off[i] .. val_off[i+1]) -> scratch[soff[i] ..), clen[i],
-// for the values i = list[0 .. *cnt).  CAP: the LDS block capacity (SE_CAP_SMALL: the values
-// <= 2 KiB, whose 7.3 KiB of LDS lets VGPRs bound the waves per CU; SE_CAP: the others,
-// 13.2 KiB; blocks longer than CAP take the lane-0 path with its table in gtables).
-template <int CAP>
-__global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
+// for the values i = list[0 .. *cnt) (*head: the work-queue head, zeroed by the caller).  CAP:
+// the LDS block capacity (SE_CAP_SMALL: the values <= 2 KiB, whose 7.3 KiB of LDS lets VGPRs
+// bound the waves per CU; SE_CAP: the others, 13.2 KiB; blocks longer than CAP take the lane-0
+// path with its table in gtables).
+template <int CAP, int WPG>
+__global__ __launch_bounds__(64 * WPG) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
                                                    const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt,
+                                                   uint32_t *__restrict__ head,
                                                    uint8_t *__restrict__ scratch, uint64_t scap,
                                                    const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
                                                    uint16_t *__restrict__ gtables) {
@@ -487,24 +495,38 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
     // The copy loop's compares read up to 67 bytes past a position < CAP: into the
     // table, never past the buffer, and clipped to the block length.
     typedef SeLayout<CAP> LY;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[LY::kWords];
+    // WPG waves per workgroup, each on its own LDS slice and its own values (no barriers):
+    // LDS is allocated per workgroup in 2-KiB granules, so 3 x 13.2 KiB fit 4 times in a CU's
+    // 160 KiB (12 waves) where single 13.2 KiB waves fit 11 times
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[WPG][LY::kWords];
+    const uint32_t wid = threadIdx.x >> 6, gw = blockIdx.x * WPG + wid, nw = gridDim.x * WPG;
+    uint32_t *lds = lds_all[wid];
     uint8_t *in = reinterpret_cast<uint8_t *>(lds);
     se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (CAP + 16) / 4);
     uint32_t *dcnt = lds + (CAP + 16) / 4 + LY::kTab * sizeof(se_tab_t) / 4;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
-    uint16_t *gt = gtables + (size_t)blockIdx.x * 16384;
+    uint16_t *gt = gtables + (size_t)gw * 16384;
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef BHG_SE_PROF
     const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
 #endif
+    // work queue: a wave's first value is list[gw] (gw: its wave index), every later one
+    // list[nw + atomicAdd(head)] -- value costs vary ~30x (length, compressibility), so a
+    // static round-robin split left the waves with the most work running alone at the end
+    // (C4 84.5 -> 98.3 GiB/s on one box).  The next index is requested when a value starts
+    // and read when it ends.  (Longest-first order within a class measured 1 % slower.)
     const uint32_t n = *cnt;
-    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+    uint32_t j = gw;
+    while (j < n) {
+        uint32_t jn = 0;
+        if (lane == 0) jn = atomicAdd(head, 1u);
         const uint32_t i = list[j];
         const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
         if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
             if (lane == 0) clen[i] = ~0ull;
+            j = BHG_SE_QUEUE ? nw + uni(jn) : j + nw;
             continue;
         }
         const uint8_t *src = vals + v0;
@@ -565,12 +587,13 @@ __global__ __launch_bounds__(64) void k_snappy_enc(const uint8_t *__restrict__ v
         }
         if (lane == 0) clen[i] = o.d;
         acc[4] += 1;
+        j = BHG_SE_QUEUE ? nw + uni(jn) : j + nw;
     }
 #ifdef BHG_SE_PROF
     acc[5] = __builtin_amdgcn_s_memtime() - t_k0;
     if (lane == 0)
         for (int q = 0; q < 8; q++) atomicAdd((unsigned long long *)&se_prof[q], (unsigned long long)acc[q]);
-    if (blockIdx.x == 0 && lane == 0)
+    if (gw == 0 && lane == 0)
         printf("se_prof wave0: scan %llu lit %llu copy %llu phases %llu values %llu total %llu batches %llu duplanes %llu\n",
                (unsigned long long)acc[0], (unsigned long long)acc[1], (unsigned long long)acc[2],
                (unsigned long long)acc[3], (unsigned long long)acc[4], (unsigned long long)acc[5],
@@ -637,39 +660,41 @@ __global__ __launch_bounds__(64 * kClassWaves) void k_enc_class(const uint64_t *
     }
 }
 
-// one wave per resident workgroup slot (LDS-bound: 13.2 KiB per wave at SE_CAP -> 11 per CU
-// with 2-KiB allocation granules; 7.3 KiB at SE_CAP_SMALL -> VGPR-bound): a grid past what is
-// resident would start its extra workgroups only when the first ones finish
-template <int CAP>
+// workgroups: as many as are resident (LDS-bound: 3 x 13.2 KiB per workgroup at SE_CAP -> 4
+// per CU with 2-KiB allocation granules; 7.3 KiB at SE_CAP_SMALL -> VGPR-bound): a grid past
+// what is resident would start its extra workgroups only when the first ones finish
+template <int CAP, int WPG>
 static uint32_t enc_grid(const Launch &L, uint32_t n) {
-    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP>, 64, BHG_SE_WAVES);
+    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP, WPG>, 64 * WPG, BHG_SE_WAVES / WPG);
     uint32_t pc = per_cu;
 #ifdef BHG_SE_MAXW  // lab: fewer resident waves per CU, to see how the encoder scales with occupancy
-    if (pc > BHG_SE_MAXW) pc = BHG_SE_MAXW;
+    if (pc * WPG > BHG_SE_MAXW) pc = BHG_SE_MAXW / WPG;
 #endif
     uint32_t g = (uint32_t)L.num_cus * pc;
-    if (g > n) g = n;
+    if ((uint64_t)g * WPG > n) g = (n + WPG - 1) / WPG;
     return g ? g : 1;
 }
 
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP>(L, n); }
+// waves of the large-value launch (one global hash table each for blocks > SE_CAP)
+uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, BHG_SE_WPG>(L, n) * BHG_SE_WPG; }
 
-size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + 2) * 4; }
+size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + 4) * 4; }
 
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
                              uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
                              uint16_t *gtables, uint32_t *lists) {
-    uint32_t *cnt = lists + 2 * (size_t)n;
-    if (hipError_t e = hipMemsetAsync(cnt, 0, 8, L.stream)) return e;
+    uint32_t *cnt = lists + 2 * (size_t)n;  // class counts cnt[0..1], queue heads cnt[2..3]
+    if (hipError_t e = hipMemsetAsync(cnt, 0, 16, L.stream)) return e;
     const uint32_t per = 64 * kClassWaves * kClassPer;
     hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
                        cnt);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL(k_snappy_enc<SE_CAP_SMALL>, dim3(enc_grid<SE_CAP_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
-                       val_off, (const uint32_t *)lists, (const uint32_t *)cnt, scratch, scap, soff, clen, gtables);
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1>), dim3(enc_grid<SE_CAP_SMALL, 1>(L, n)), dim3(64), 0, L.stream, vals,
+                       val_off, (const uint32_t *)lists, cnt, cnt + 2, scratch, scap, soff, clen, gtables);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL(k_snappy_enc<SE_CAP>, dim3(enc_grid<SE_CAP>(L, n)), dim3(64), 0, L.stream, vals, val_off,
-                       (const uint32_t *)lists + n, (const uint32_t *)cnt + 1, scratch, scap, soff, clen, gtables);
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG>), dim3(enc_grid<SE_CAP, BHG_SE_WPG>(L, n)), dim3(64 * BHG_SE_WPG), 0,
+                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 3, scratch, scap, soff, clen,
+                       gtables);
     return hipGetLastError();
 }
 
