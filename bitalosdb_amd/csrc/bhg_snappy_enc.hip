@@ -31,6 +31,9 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_WPG
 #define BHG_SE_WPG 3    // waves per workgroup of the large-value launch
 #endif
+#ifndef BHG_SE_UNI
+#define BHG_SE_UNI 1
+#endif
 #ifndef BHG_SE_WAVES
 #define BHG_SE_WAVES 7
 #endif
@@ -131,6 +134,9 @@ __device__ __forceinline__ void se_emit_copy(Out &o, uint32_t offset, uint32_t l
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// ballot of a bool straight from its compare (HIP's bal(int) re-materialises the bool in a
+// VGPR and compares it again: two VALU per ballot)
+__device__ __forceinline__ uint64_t bal(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 // order LDS accesses of this wave (no instruction: LDS executes a wave's ops in order)
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
@@ -200,7 +206,7 @@ __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, u
         }
     }
     // literal bytes: one op at a time, 64 bytes per wave instruction
-    uint64_t lm = __ballot(lit != 0);
+    uint64_t lm = bal(lit != 0);
     while (lm) {
         const uint32_t k = (uint32_t)__builtin_ctzll(lm);
         lm &= lm - 1;
@@ -215,12 +221,25 @@ __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, u
 
 // op n of the ring (the caller flushes a full ring before the next push): three selects,
 // no exec-mask branch, nothing on the matcher's dependency chain
+// v with lane i := x (x, i wave-uniform): the v_writelane_b32 intrinsic (no clang builtin here)
+extern "C" __device__ int bhg_llvm_writelane(int x, int i, int v) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t wlane(uint32_t v, uint32_t x, uint32_t i) {
+    return (uint32_t)bhg_llvm_writelane((int)x, (int)i, (int)v);
+}
 __device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t s, uint32_t e, uint32_t c) {
+#if BHG_SE_UNI
+    // s, e, c, r.n are wave-uniform: one v_writelane each
+    r.s = wlane(r.s, s, r.n);
+    r.e = wlane(r.e, e, r.n);
+    r.c = wlane(r.c, c, r.n);
+    r.n = uni(r.n + 1);
+#else
     const bool mine = lane == r.n;
     r.s = mine ? s : r.s;
     r.e = mine ? e : r.e;
     r.c = mine ? c : r.c;
     r.n++;
+#endif
 }
 
 // lane i <- lane i + 1 (DPP wave_shl:1; lane 63 gets 0)
@@ -245,7 +264,7 @@ __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, c
 // m_js, whether it is a match.
 template <uint32_t DUMMY>
 __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
-                                             uint32_t nl, bool valid, uint32_t pos, uint32_t u, uint32_t h,
+                                             uint32_t nl, bool valid, uint64_t vmask, uint32_t pos, uint32_t u, uint32_t h,
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
     // lanes that may share a bucket: per-bucket counts of h mod 1024, one byte per bucket
     // (<= 64 adds per byte); only those lanes are walked
@@ -256,7 +275,10 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
     const uint32_t cnt = dcnt[slot];
     wsync();
     atomicSub(&dcnt[slot], one);
-    const uint64_t dm0 = __ballot(valid && ((cnt >> sh8) & 0xffu) > 1);
+    // (lane predicates combined as 64-bit masks: a ballot of a combined bool re-materialises it
+    // in a VGPR, two VALU each)
+    const uint64_t vm = vmask;
+    const uint64_t dm0 = vm & bal(((cnt >> sh8) & 0xffu) > 1);
 #ifdef BHG_SE_PROF
     acc[6] += 1;
     acc[7] += __builtin_popcountll(dm0);
@@ -271,18 +293,20 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
         const uint32_t i = (uint32_t)__builtin_ctzll(dm);
         dm &= dm - 1;
         const uint32_t hi = lane_val(h, i), pi = lane_val(pos, i);
-        const uint64_t above = __ballot(h == hi) & (~1ull << i);   // lanes > i with hash hi
-        if ((above >> lane) & 1) c = pi;
-        if (lane == i) nxt = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+        const bool same = h == hi;
+        const uint64_t above = bal(same) & (~1ull << i);   // lanes > i with hash hi
+        c = same && lane > i ? pi : c;
+        nxt = wlane(nxt, above ? (uint32_t)__builtin_ctzll(above) : 64u, i);
     }
-    if (__ballot(c != c0)) eq = ld32a(in32, c) == u;
-    const bool m = valid && eq;
-    const uint64_t ev = __ballot(lane < nl && (!valid || m));
+    uint64_t em = bal(eq);
+    if (bal(c != c0)) em = bal(ld32a(in32, c) == u);
+    const uint64_t mb = vm & em;  // matches
+    const uint64_t ev = (nl >= 64 ? ~0ull : ((1ull << nl) - 1ull)) & (~vm | mb);
     const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
-    m_js = js < 64 && lane_val((uint32_t)m, js) != 0;
+    const uint32_t mj = (uint32_t)__builtin_popcountll(mb & ev & (0ull - ev));  // the event lane's match bit
+    m_js = mj != 0;
     // updating iterations: the lanes before the event, and the event itself when it is a match
-    uint32_t nu = js + (m_js ? 1u : 0u);
-    if (nu > nl) nu = nl;
+    const uint32_t nu = min(js + mj, nl);
     tab[lane < nu && nxt >= nu ? h : DUMMY + lane] = (se_tab_t)pos;   // others: a scratch slot each
     wsync();
     return js;
@@ -294,8 +318,14 @@ template <uint32_t DUMMY>
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                              uint32_t f0, uint32_t f0n, uint64_t *acc) {
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
+#if BHG_SE_UNI
+    len = uni(len);
+#endif
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
+#if BHG_SE_UNI
+    shift = uni(shift);
+#endif
     const uint32_t tmask = 16383;
     const uint32_t sLimit = len - SE_MARGIN;
     uint32_t nextEmit = 0, s = 1;
@@ -321,11 +351,13 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // 4-byte check of that entry is issued with the duplicate count
             const uint32_t u = lane_next(Uw), h = lane_next(hUw);
             uint32_t c = lane_next(tUw);
-            const bool valid = lane <= 32 && s + (lane < 32 ? lane + 1 : 34u) <= sLimit;
+            const bool inl = s + (lane < 32 ? lane + 1 : 34u) <= sLimit;
+            const bool valid = lane <= 32 && inl;
+            const uint64_t vmask = bal(inl) & ((2ull << 32) - 1ull);
             const uint32_t pos = s + lane;
             const bool eq = ld32a(in32, valid ? c : 0u) == u;
             bool m;
-            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 33, valid, pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 33, valid, vmask, pos, u, h, c, eq, m, acc);
             if (js < 33) {
                 found = true;
                 if (!m) remainder = true;
@@ -338,8 +370,10 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // constant table (a global load: it waits for the flushed output stores too)
             uint32_t fk = f0, fk1 = f0n;
             if (kb != 0) {
-                fk = kb + lane < 1025 ? kSkip.f[kb + lane] : 0x7fffffffu;
-                fk1 = kb + lane + 1 < 1025 ? kSkip.f[kb + lane + 1] : 0x7fffffffu;
+                // clamped, unconditional loads (F[1024] is the 2^31 - 1 sentinel; a <= 4 KiB
+                // block's scan ends by k = 177)
+                fk = kSkip.f[min(kb + lane, 1024u)];
+                fk1 = kSkip.f[min(kb + lane + 1, 1024u)];
             }
             // s < 64 Ki and F[k] <= 2^31 - 1: the sums fit in 32 bits
             const bool valid = s + fk1 <= sLimit;
@@ -349,7 +383,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
             const bool eq = ld32a(in32, c) == u;
             bool m;
-            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 64, valid, pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 64, valid, bal(valid), pos, u, h, c, eq, m, acc);
             if (js < 64) {
                 found = true;
                 if (!m) remainder = true;
@@ -372,12 +406,23 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         // prevHash == currHash is resolved by a compare.  So the lookup costs no LDS round
         // trip after the compare; copies ending at s + 64 or later take a serial lookup.
         for (;;) {
+#if BHG_SE_UNI
+            // s, cand are wave-uniform; the compiler's divergence analysis cannot see it through
+            // the loop's phis and kept them (and everything computed from them) in VGPRs
+            s = uni(s);
+            cand = uni(cand);
+#endif
             const uint32_t U = ld32a(in32, s + lane);
             const uint32_t V = in[cand + lane];
             const uint32_t hU = se_hash(U, shift) & tmask;
             const uint32_t tU = tab[hU];
-            const uint64_t mm = __ballot((U & 0xffu) != V);
+            const uint64_t mm = bal((U & 0xffu) != V);
+#if BHG_SE_UNI
+            // the first mismatch lane (64: none) as a scalar, so the mins stay SALU
+            uint32_t f = min(uni(mm ? (uint32_t)__builtin_ctzll(mm) : 64u), len - s);
+#else
             uint32_t f = min(mm ? (uint32_t)__builtin_ctzll(mm) : 64u, len - s);
+#endif
             if (f < 4u) {  // the chained candidate does not match: scanning resumes at s + 1
                 Uw = U;
                 hUw = hU;
@@ -387,8 +432,12 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             uint32_t r0 = s;  // start of the round that found the mismatch
             while (f == 64u) {
                 r0 += 64;
-                const uint64_t m2 = __ballot(in[r0 + lane] != in[cand + (r0 - s) + lane]);
+                const uint64_t m2 = bal(in[r0 + lane] != in[cand + (r0 - s) + lane]);
+#if BHG_SE_UNI
+                f = min(uni(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u), len - r0);
+#else
                 f = min(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u, len - r0);
+#endif
             }
             const uint32_t e = r0 + f;
             se_push(r, lane, s, e, cand);
@@ -411,7 +460,16 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // the slots coincide both lanes store s)
             const bool same = prevHash == currHash;
             wsync();
+#if BHG_SE_UNI
+            // lane 0 stores s - 1 (s when the slots coincide) at prevHash, lane 1 s at currHash,
+            // the others s into their scratch slots: two v_writelane per operand
+            {
+                const uint32_t ad = wlane(wlane(DUMMY + lane, prevHash, 0), currHash, 1);
+                tab[ad] = (se_tab_t)wlane(s, same ? s : s - 1, 0);
+            }
+#else
             tab[lane == 0 ? prevHash : lane == 1 ? currHash : DUMMY + lane] = (se_tab_t)(lane || same ? s : s - 1);
+#endif
             cand = same ? s - 1 : tc;
             wsync();
             if (r.n == 64) se_flush(o, in, r, lane);
