@@ -62,13 +62,15 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes that measure roofline.traffic (N=1, rank 0)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "scan", "scanmix", "get",
-                                                       "indexcrc"],
+                                                       "indexcrc", "spawncheck"],
                     help="c1: 100k blocks on the host CPU; c2: uncompressed decode (BASELINE metric; at N > 1 "
                          "the line is the C5 strong-scaling corpus); c3: snappy decode; c4: encode; "
                          "c5: 25 GB corpus sharded round-robin by table over the GPUs (strong scaling); "
                          "scan/scanmix: table data-region scan over uniform / mixed-length tables; "
                          "get: batched Bithash.Get (HashIndex + conflict SeekGE + readData) over full tables; "
-                         "indexcrc: per-table indexhash_checksum verify (masked CRC-32C of 1.51 MB per table)")
+                         "indexcrc: per-table indexhash_checksum verify (masked CRC-32C of 1.51 MB per table); "
+                         "spawncheck: no GPU -- the --gpus N launch path alone (rank env, gloo rendezvous, "
+                         "the all-reduce that reports ranks_seen, rank 0's JSON line), for CPU tests")
     return ap.parse_args()
 
 
@@ -286,6 +288,8 @@ def main():
         print("bench.py: --gpus %d but WORLD_SIZE %d" % (a.gpus, world), file=sys.stderr)
         sys.exit(2)
     import torch.distributed as dist
+    if a.config == "spawncheck":
+        return spawn_check(a, world, rank)
     global BACKEND
     BACKEND = a.backend
     if a.backend == "gloo":   # rehearsal: ranks may share a GPU
@@ -308,6 +312,20 @@ def main():
     codec.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def spawn_check(a, world, rank):
+    """--config spawncheck: the multi-rank launch path without a GPU.  Every rank joins a
+    gloo group and all-reduces 1 and its rank; rank 0 prints what it saw."""
+    import torch.distributed as dist
+    t = torch.tensor([1, rank], dtype=torch.int64)
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.all_reduce(t)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"config": "spawncheck", "n_gpus": world, "ranks_seen": int(t[0]),
+                          "rank_sum": int(t[1]), "spawned": os.environ.get("BHG_BENCH_SPAWNED") == "1"}), flush=True)
 
 
 def run(a, world, rank, local, dev, codec):

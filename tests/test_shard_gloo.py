@@ -107,3 +107,35 @@ def test_single_process_reduce():
     import torch
     el, ok, n, dg = shard.reduce_stats(1.25, 7, 8, (5 << 32) | 9, torch.device("cpu"))
     assert (el, ok, n, dg) == (1.25, 7, 8, (5 << 32) | 9)
+
+
+def _bench(args, env_extra=None, timeout=180):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, cwd=root,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_self_spawn_world2():
+    """`bench.py --gpus 2` with no outer launcher (how the driver runs it): bench.py starts
+    the two rank processes itself, they rendezvous over gloo and all-reduce, and rank 0's
+    JSON line reports n_gpus 2 and ranks_seen 2 (--config spawncheck: the launch path
+    without a GPU; the GPU lines run the same spawn_ranks / main code first)."""
+    import json
+    r = _bench(["--gpus", "2", "--backend", "gloo", "--config", "spawncheck"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d == {"config": "spawncheck", "n_gpus": 2, "ranks_seen": 2, "rank_sum": 1, "spawned": True}
+
+
+def test_bench_gpus_must_match_world_size():
+    """--gpus N under an outer launcher whose WORLD_SIZE differs is an error (exit 2)."""
+    r = _bench(["--gpus", "2", "--config", "spawncheck"], {"WORLD_SIZE": "3", "RANK": "0"}, timeout=120)
+    assert r.returncode == 2 and "--gpus 2 but WORLD_SIZE 3" in r.stderr
