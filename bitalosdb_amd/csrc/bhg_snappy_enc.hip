@@ -34,6 +34,9 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_UNI
 #define BHG_SE_UNI 1
 #endif
+#ifndef BHG_SE_MINW_SMALL
+#define BHG_SE_MINW_SMALL 4  // waves per SIMD the small-value kernel is compiled for (VGPR budget)
+#endif
 #ifndef BHG_SE_WAVES
 #define BHG_SE_WAVES 7
 #endif
@@ -542,8 +545,8 @@ rem:
 // the LDS block capacity (SE_CAP_SMALL: the values <= 2 KiB, whose 7.3 KiB of LDS lets VGPRs
 // bound the waves per CU; SE_CAP: the others, 13.2 KiB; blocks longer than CAP take the lane-0
 // path with its table in gtables).
-template <int CAP, int WPG>
-__global__ __launch_bounds__(64 * WPG) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
+template <int CAP, int WPG, int MINW>
+__global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
                                                    const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt,
                                                    uint32_t *__restrict__ head,
                                                    uint8_t *__restrict__ scratch, uint64_t scap,
@@ -721,9 +724,9 @@ __global__ __launch_bounds__(64 * kClassWaves) void k_enc_class(const uint64_t *
 // workgroups: as many as are resident (LDS-bound: 3 x 13.2 KiB per workgroup at SE_CAP -> 4
 // per CU with 2-KiB allocation granules; 7.3 KiB at SE_CAP_SMALL -> VGPR-bound): a grid past
 // what is resident would start its extra workgroups only when the first ones finish
-template <int CAP, int WPG>
+template <int CAP, int WPG, int MINW>
 static uint32_t enc_grid(const Launch &L, uint32_t n) {
-    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP, WPG>, 64 * WPG, BHG_SE_WAVES / WPG);
+    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP, WPG, MINW>, 64 * WPG, BHG_SE_WAVES / WPG);
     uint32_t pc = per_cu;
 #ifdef BHG_SE_MAXW  // lab: fewer resident waves per CU, to see how the encoder scales with occupancy
     if (pc * WPG > BHG_SE_MAXW) pc = BHG_SE_MAXW / WPG;
@@ -734,7 +737,7 @@ static uint32_t enc_grid(const Launch &L, uint32_t n) {
 }
 
 // waves of the large-value launch (one global hash table each for blocks > SE_CAP)
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, BHG_SE_WPG>(L, n) * BHG_SE_WPG; }
+uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n) * BHG_SE_WPG; }
 
 size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + 4) * 4; }
 
@@ -747,10 +750,10 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
     hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
                        cnt);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1>), dim3(enc_grid<SE_CAP_SMALL, 1>(L, n)), dim3(64), 0, L.stream, vals,
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>), dim3(enc_grid<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
                        val_off, (const uint32_t *)lists, cnt, cnt + 2, scratch, scap, soff, clen, gtables);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG>), dim3(enc_grid<SE_CAP, BHG_SE_WPG>(L, n)), dim3(64 * BHG_SE_WPG), 0,
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG, 3>), dim3(enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n)), dim3(64 * BHG_SE_WPG), 0,
                        L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 3, scratch, scap, soff, clen,
                        gtables);
     return hipGetLastError();
