@@ -579,20 +579,56 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     // (C4 84.5 -> 98.3 GiB/s on one box).  The next index is requested when a value starts
     // and read when it ends.  (Longest-first order within a class measured 1 % slower.)
     const uint32_t n = *cnt;
+    // Positions are pipelined so that no value waits for its own bookkeeping: while value j
+    // runs, the next position's list entry i1 is known and its offsets (m1) are loaded, and
+    // the position after it (j2) is taken from the queue and its list entry loaded -- issued
+    // once this value's bytes are staged (the staging round trip covers the queue atomic).
+    // Before, every value started with three dependent round trips (list, offsets, bytes).
+    struct Meta {
+        uint32_t i;
+        uint64_t v0, v1, s0, s1;
+    };
+    auto meta_of = [&](uint32_t jj, uint32_t ii) {
+        Meta m = {ii, 0, 0, 0, 0};
+        if (jj < n) {
+            m.v0 = val_off[ii];
+            m.v1 = val_off[ii + 1];
+            m.s0 = soff[ii];
+            m.s1 = soff[ii + 1];
+        }
+        return m;
+    };
+    auto take = [&](uint32_t cur, uint32_t req) { return BHG_SE_QUEUE ? nw + uni(req) : cur + nw; };
     uint32_t j = gw;
+    Meta mc = meta_of(j, j < n ? list[j] : 0u);
+    uint32_t r0 = 0;
+    if (lane == 0) r0 = atomicAdd(head, 1u);
+    uint32_t j1 = take(j, r0);
+    uint32_t i1 = j1 < n ? list[j1] : 0u;
     while (j < n) {
-        uint32_t jn = 0;
-        if (lane == 0) jn = atomicAdd(head, 1u);
-        const uint32_t i = list[j];
-        const uint64_t v0 = val_off[i], vlen = val_off[i + 1] - v0;
-        if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
+        uint32_t rq = 0;
+        if (lane == 0) rq = atomicAdd(head, 1u);  // the position after j1
+        uint32_t j2 = 0, i2 = 0;
+        Meta m1 = {0, 0, 0, 0, 0};
+        bool hooked = false;
+        auto hook = [&]() {  // once per value, after its bytes are staged
+            if (hooked) return;
+            hooked = true;
+            j2 = take(j1, rq);
+            i2 = j2 < n ? list[j2] : 0u;
+            m1 = meta_of(j1, i1);
+        };
+        const uint32_t i = mc.i;
+        const uint64_t v0 = mc.v0, vlen = mc.v1 - mc.v0;
+        if (mc.s1 > scap) {  // val_off inconsistent with the vals_len the caller passed
             if (lane == 0) clen[i] = ~0ull;
-            j = BHG_SE_QUEUE ? nw + uni(jn) : j + nw;
+            hook();
+            j = j1; j1 = j2; i1 = i2; mc = m1;
             continue;
         }
         const uint8_t *src = vals + v0;
         Out o;
-        o.g = scratch + soff[i];
+        o.g = scratch + mc.s0;
         o.d = 0;
         // uvarint(len(src))
         {
@@ -635,6 +671,7 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
                 for (uint32_t t = 8 * lane; t < ts; t += 512)   // 16 B per lane per store (ts >= 256)
                     *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
                 wsync();
+                hook();
                 se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
             } else {
                 uint32_t d = o.d;
@@ -646,9 +683,13 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
                 o.d = uni(d);
             }
         }
+        hook();  // (values with no LDS block)
         if (lane == 0) clen[i] = o.d;
         acc[4] += 1;
-        j = BHG_SE_QUEUE ? nw + uni(jn) : j + nw;
+        j = j1;
+        j1 = j2;
+        i1 = i2;
+        mc = m1;
     }
 #ifdef BHG_SE_PROF
     acc[5] = __builtin_amdgcn_s_memtime() - t_k0;

@@ -18,6 +18,10 @@ timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --warmup 5 > $O/ben
 for c in c3 c4; do
   timeout -k 10 300 python -u bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { echo "bench $c failed"; exit 1; }
 done
+timeout -k 10 300 python -u bench.py --config c5 --codec snappy --no-cpu > $O/bench_c5_snappy.json 2> $O/bench_c5_snappy.err || { echo "bench c5 snappy failed"; exit 1; }
+for c in get indexcrc; do
+  timeout -k 10 300 python -u bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { echo "bench $c failed"; exit 1; }
+done
 for f in $O/bench_*.json; do python -c "
 import json; d=json.load(open('$f')); r=d.get('roofline',{})
 print('$f'.split('/')[-1], d['n_gpus'], d['value'], d['unit'], d['ms_per_step'], r.get('frac'), r.get('traffic_ratio'), d.get('valid'), d.get('strong_c5',{}).get('value'))"; done
