@@ -141,6 +141,23 @@ def test_encode_snappy_byte_exact(codec, seed):
         assert dv[int(doff[i]):int(doff[i + 1])].tobytes() == vals[i]
 
 
+@pytest.mark.parametrize("sizes", [[0], [3000], [100, 3000], [2048, 2049], [4096] * 7, [1500] * 65,
+                                   [5000, 17, 2048, 4097, 0, 64]])
+def test_encode_snappy_tiny_batches(codec, sizes):
+    """The encoder's class lists and work queue at batch sizes far below the grid:
+    one value, empty small or large list, the 2 KiB / 4 KiB class edges, a class
+    list longer than one wave's first take (the queue hands out the rest) --
+    byte-exact with the restatement."""
+    rng = random.Random(len(sizes) * 7 + sizes[0])
+    n = len(sizes)
+    keys = [rb(rng, 24) for _ in range(n)]
+    vals = [compressible(rng, sz) if i % 2 == 0 else rb(rng, sz) for i, sz in enumerate(sizes)]
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    got = codec.encode(keys, tr, vals, compressor=1, file_nums=[5, 6], table_max=1 << 20)
+    exp = O.encode_batch(keys, tr, vals, codec=1, file_nums=[5, 6], table_max=1 << 20)
+    check(got, exp)
+
+
 def test_encode_out_cap_too_small(codec):
     """Records that end past out_cap are not written: status NO_SPACE, pos
     UINT64_MAX, counted in summary[2]; summary[0] still reports the bytes the
