@@ -28,6 +28,9 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_QUEUE
 #define BHG_SE_QUEUE 1  // values handed to waves by a work queue (0: static round-robin, lab)
 #endif
+#ifndef BHG_SE_STATIC
+#define BHG_SE_STATIC 75  // % of a class list handed out round-robin before the work queue takes over
+#endif
 #ifndef BHG_SE_WPG
 #define BHG_SE_WPG 3    // waves per workgroup of the large-value launch
 #endif
@@ -598,16 +601,21 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
         }
         return m;
     };
-    auto take = [&](uint32_t cur, uint32_t req) { return BHG_SE_QUEUE ? nw + uni(req) : cur + nw; };
+    // the first BHG_SE_STATIC % of the list goes round-robin (position cur + nw, no atomic: a
+    // queue atomic per value made every wave contend on one address), the rest through the
+    // queue (positions qbase + head++), which evens out the end of the launch
+    const uint32_t qbase = BHG_SE_QUEUE ? (uint32_t)((uint64_t)n * BHG_SE_STATIC / 100 / nw * nw) : 0xffffffffu;
+    auto need_q = [&](uint32_t cur) { return cur + nw >= qbase; };
+    auto take = [&](uint32_t cur, uint32_t req) { return need_q(cur) ? max(qbase, nw) + uni(req) : cur + nw; };
     uint32_t j = gw;
     Meta mc = meta_of(j, j < n ? list[j] : 0u);
     uint32_t r0 = 0;
-    if (lane == 0) r0 = atomicAdd(head, 1u);
+    if (lane == 0 && need_q(j)) r0 = atomicAdd(head, 1u);
     uint32_t j1 = take(j, r0);
     uint32_t i1 = j1 < n ? list[j1] : 0u;
     while (j < n) {
         uint32_t rq = 0;
-        if (lane == 0) rq = atomicAdd(head, 1u);  // the position after j1
+        if (lane == 0 && need_q(j1)) rq = atomicAdd(head, 1u);  // the position after j1
         uint32_t j2 = 0, i2 = 0;
         Meta m1 = {0, 0, 0, 0, 0};
         bool hooked = false;
