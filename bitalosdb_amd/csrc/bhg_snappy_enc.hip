@@ -28,6 +28,9 @@ typedef u32x4 u32x4u __attribute__((aligned(1)));
 #ifndef BHG_SE_QUEUE
 #define BHG_SE_QUEUE 1  // values handed to waves by a work queue (0: static round-robin, lab)
 #endif
+#ifndef BHG_SE_HEADS
+#define BHG_SE_HEADS 8  // queue heads per class list
+#endif
 #ifndef BHG_SE_STATIC
 #define BHG_SE_STATIC 75  // % of a class list handed out round-robin before the work queue takes over
 #endif
@@ -606,16 +609,23 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     // queue (positions qbase + head++), which evens out the end of the launch
     const uint32_t qbase = BHG_SE_QUEUE ? (uint32_t)((uint64_t)n * BHG_SE_STATIC / 100 / nw * nw) : 0xffffffffu;
     auto need_q = [&](uint32_t cur) { return cur + nw >= qbase; };
-    auto take = [&](uint32_t cur, uint32_t req) { return need_q(cur) ? max(qbase, nw) + uni(req) : cur + nw; };
+    // BHG_SE_HEADS queue heads, 128 B apart: wave gw takes from head gw mod H, whose positions are
+    // qstart + h + H k (the waves of one head are an interleaved H-th of the grid, its positions
+    // an interleaved H-th of the queued part: balanced, and H times fewer atomics per address)
+    const uint32_t hq = gw % BHG_SE_HEADS;
+    uint32_t *const myhead = head + 32 * hq;
+    auto take = [&](uint32_t cur, uint32_t req) {
+        return need_q(cur) ? max(qbase, nw) + hq + BHG_SE_HEADS * uni(req) : cur + nw;
+    };
     uint32_t j = gw;
     Meta mc = meta_of(j, j < n ? list[j] : 0u);
     uint32_t r0 = 0;
-    if (lane == 0 && need_q(j)) r0 = atomicAdd(head, 1u);
+    if (lane == 0 && need_q(j)) r0 = atomicAdd(myhead, 1u);
     uint32_t j1 = take(j, r0);
     uint32_t i1 = j1 < n ? list[j1] : 0u;
     while (j < n) {
         uint32_t rq = 0;
-        if (lane == 0 && need_q(j1)) rq = atomicAdd(head, 1u);  // the position after j1
+        if (lane == 0 && need_q(j1)) rq = atomicAdd(myhead, 1u);  // the position after j1
         uint32_t j2 = 0, i2 = 0;
         Meta m1 = {0, 0, 0, 0, 0};
         bool hooked = false;
@@ -788,22 +798,24 @@ static uint32_t enc_grid(const Launch &L, uint32_t n) {
 // waves of the large-value launch (one global hash table each for blocks > SE_CAP)
 uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n) * BHG_SE_WPG; }
 
-size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + 4) * 4; }
+// class lists (2n), class counts (4 words), then 2 x BHG_SE_HEADS queue heads of 32 words each
+constexpr uint32_t kQueueWords = 4 + 2 * BHG_SE_HEADS * 32;
+size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + kQueueWords) * 4; }
 
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
                              uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
                              uint16_t *gtables, uint32_t *lists) {
-    uint32_t *cnt = lists + 2 * (size_t)n;  // class counts cnt[0..1], queue heads cnt[2..3]
-    if (hipError_t e = hipMemsetAsync(cnt, 0, 16, L.stream)) return e;
+    uint32_t *cnt = lists + 2 * (size_t)n;  // class counts cnt[0..1], queue heads from cnt + 4
+    if (hipError_t e = hipMemsetAsync(cnt, 0, kQueueWords * 4, L.stream)) return e;
     const uint32_t per = 64 * kClassWaves * kClassPer;
     hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
                        cnt);
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>), dim3(enc_grid<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
-                       val_off, (const uint32_t *)lists, cnt, cnt + 2, scratch, scap, soff, clen, gtables);
+                       val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen, gtables);
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG, 3>), dim3(enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n)), dim3(64 * BHG_SE_WPG), 0,
-                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 3, scratch, scap, soff, clen,
+                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * BHG_SE_HEADS, scratch, scap, soff, clen,
                        gtables);
     return hipGetLastError();
 }
