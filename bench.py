@@ -57,6 +57,11 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--codec", default="none", choices=["none", "snappy"], help="c5 only")
+    ap.add_argument("--values", default="dict", choices=["dict", "chunk16"], help="c3/c4/c5-snappy values: " +
+                    "dict: SURVEY 8(d)'s token generator (the primary workload); chunk16: 16-B chunks of 8 per-value "
+                    "random words")
+    ap.add_argument("--no-secondary", action="store_true", help="c3/c4: skip the nested line of the other value "
+                                                                  "generator")
     ap.add_argument("--c5-tables", type=int, default=184, help="c5 corpus size in 128 MiB tables")
     ap.add_argument("--no-c5", action="store_true", help="N=1: skip the nested strong_c5 record")
     ap.add_argument("--no-traffic", action="store_true",
@@ -119,9 +124,10 @@ PMC_PASSES = (("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_
 
 
 def measure_traffic(config_args, kernels, timeout_s=240):
-    """{kernel prefix: median HBM bytes per launch (read, write)} from two rocprofv3 --pmc passes of
-    `bench.py <config_args> --steps 2 --warmup 1`; None (with the reason) when the profiler is
-    missing or a pass fails."""
+    """{full kernel name: median HBM bytes per launch (read, write)} for every kernel whose name
+    contains one of `kernels`, from two rocprofv3 --pmc passes of `bench.py <config_args> --steps 2
+    --warmup 1`; None (with the reason) when the profiler is missing or a pass fails.  Each kernel
+    listed runs once per step, so the sum over the result is the step's traffic."""
     import csv
     import glob
     import shutil
@@ -134,7 +140,6 @@ def measure_traffic(config_args, kernels, timeout_s=240):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     per = {}   # (kernel, dispatch) -> {counter: value}
-    names = {}
     with tempfile.TemporaryDirectory(prefix="bhg_pmc_", dir=env["TMPDIR"]) as td:
         for i, counters in enumerate(PMC_PASSES):
             out = os.path.join(td, "p%d" % i)
@@ -156,21 +161,22 @@ def measure_traffic(config_args, kernels, timeout_s=240):
             for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
                 for row in csv.DictReader(open(f)):
                     kn = row["Kernel_Name"]
-                    hit = [k for k in kernels if k in kn]
-                    if not hit:
+                    if not any(k in kn for k in kernels):
                         continue
-                    key = (hit[0], i, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+                    # keyed by the FULL kernel name (template arguments included): two instantiations
+                    # of one template (k_snappy_enc<2048, ..> and <4096, ..>) are two kernels of the step
+                    full = kn.split("(")[0].strip()
+                    key = (full, i, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
                     per.setdefault(key, {})[row["Counter_Name"]] = float(row["Counter_Value"])
-                    names[hit[0]] = kn.split("(")[0]
     res = {}
-    for k in kernels:
+    for full in sorted({kk for (kk, _, _) in per}):
         rd = [32 * c.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) +
-              128 * c.get("TCC_EA0_RDREQ_128B_sum", 0) for (kk, i, _), c in per.items() if kk == k and i == 0]
+              128 * c.get("TCC_EA0_RDREQ_128B_sum", 0) for (kk, i, _), c in per.items() if kk == full and i == 0]
         wr = [32 * (c.get("TCC_EA0_WRREQ_sum", 0) - c.get("TCC_EA0_WRREQ_64B_sum", 0)) +
-              64 * c.get("TCC_EA0_WRREQ_64B_sum", 0) for (kk, i, _), c in per.items() if kk == k and i == 1]
+              64 * c.get("TCC_EA0_WRREQ_64B_sum", 0) for (kk, i, _), c in per.items() if kk == full and i == 1]
         if rd and wr:
-            res[k] = {"read": float(np.median(rd)), "write": float(np.median(wr)), "launches": min(len(rd), len(wr)),
-                      "name": names.get(k, k)}
+            res[full] = {"read": float(np.median(rd)), "write": float(np.median(wr)), "launches": min(len(rd), len(wr)),
+                         "name": full}
     if not res:
         return None, "no dispatch of %s in the pmc passes" % ",".join(kernels)
     return res, None
@@ -187,7 +193,7 @@ def traffic_fields(cfg_args, kernels, alg_bytes_per_launch, what):
     tot = sum(v["read"] + v["write"] for v in res.values())
     return {"traffic": round(tot), "traffic_ratio": round(tot / alg_bytes_per_launch, 4),
             "traffic_source": "measured in this run: bench.py %s under rocprofv3 --pmc (%s | %s), median per "
-                              "launch of %s; HBM bytes = 32/64/128-B read requests + 32/64-B write requests at "
+                              "launch of each kernel, summed over %s (each runs once per step); HBM bytes = 32/64/128-B read requests + 32/64-B write requests at "
                               "the L2 fabric interface; algorithmic bytes per launch %d (%s)" % (
                                   " ".join(cfg_args), " ".join(PMC_PASSES[0]), " ".join(PMC_PASSES[1]),
                                   ", ".join(v["name"] for v in res.values()), alg_bytes_per_launch, what),
@@ -318,14 +324,19 @@ def spawn_check(a, world, rank):
     """--config spawncheck: the multi-rank launch path without a GPU.  Every rank joins a
     gloo group and all-reduces 1 and its rank; rank 0 prints what it saw."""
     import torch.distributed as dist
+    from bitalosdb_amd import shard
     t = torch.tensor([1, rank], dtype=torch.int64)
     if world > 1:
         dist.init_process_group("gloo")
         dist.all_reduce(t)
+    # the N > 1 line's self-describing fields, from the same helper c5_measure uses (dummy timings)
+    sf = shard.scaling_fields(1.0 + 0.5 * rank, 0.5, torch.device("cpu"))
+    if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({"config": "spawncheck", "n_gpus": world, "ranks_seen": int(t[0]),
-                          "rank_sum": int(t[1]), "spawned": os.environ.get("BHG_BENCH_SPAWNED") == "1"}), flush=True)
+                          "rank_sum": int(t[1]), "spawned": os.environ.get("BHG_BENCH_SPAWNED") == "1",
+                          "scaling_fields": sf}), flush=True)
 
 
 def run(a, world, rank, local, dev, codec):
@@ -615,16 +626,16 @@ def _pack_values(vals_t):
     return vals_t.reshape(-1).contiguous(), off
 
 
-def _encode_inputs(n, val_lens, dev, seed):
-    """Keys/trailers/values for n pairs (values from the compressible generator)."""
+def _encode_inputs(n, val_lens, dev, seed, gen):
+    """Keys/trailers/values for n pairs (values from the compressible generator `gen`)."""
     from bitalosdb_amd import synth
-    return synth.kv_pairs_gpu(n, val_lens, device=dev, seed=seed)
+    return synth.kv_pairs_gpu(n, val_lens, device=dev, seed=seed, gen=gen)
 
 
-def _encode_tables(codec, n, val_lens, dev, seed, compressor):
+def _encode_tables(codec, n, val_lens, dev, seed, compressor, gen="dict"):
     """Encode n pairs into bithash tables on the GPU; returns (src, handles, meta, raw_bytes)."""
     from bitalosdb_amd.codec import EncodeBuffers, HANDLE_DT
-    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, seed)
+    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, seed, gen)
     cap = int(n * 64 + vals.numel() * 7 // 6 + 64)
     out = torch.empty(cap, dtype=torch.uint8, device=dev)
     maxt = 4096
@@ -657,51 +668,80 @@ def _timed(a, dev, fn):
     return el, float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
 
+def _secondary_gen(gen):
+    from bitalosdb_amd import synth
+    return [g for g in synth.VALUE_GENS if g != gen][0]
+
+
 def run_c3(a, world, rank, local, dev, codec):
-    """BASELINE configs[2]: 1M snappy blocks, full CRC + decompress + decode, 32 B / 1 KiB."""
+    """BASELINE configs[2]: 1M snappy blocks, full CRC (against the writer's CRCs) + decompress +
+    decode, 32 B / 1 KiB.  The line is the --values generator (default: SURVEY 8(d)'s dictionary
+    generator); the other generator is nested as a secondary line."""
+    out = c3_measure(a, world, rank, local, dev, codec, a.values, extras=True)
+    if not a.no_secondary:
+        torch.cuda.empty_cache()
+        g2 = _secondary_gen(a.values)
+        sec = c3_measure(a, world, rank, local, dev, codec, g2, extras=False)
+        out["secondary_values_" + g2] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "roofline",
+                                                              "status_ok_blocks")}
+        out["secondary_values_" + g2].update(sec["config"])
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def c3_measure(a, world, rank, local, dev, codec, gen, extras):
     n = a.blocks
     val_lens = torch.full((n,), 1024, dtype=torch.int64, device=dev)
-    src, h, meta, _ = _encode_tables(codec, n, val_lens, dev, synth_seed(rank), 1)
+    src, h, meta, enc = _encode_tables(codec, n, val_lens, dev, synth_seed(rank), 1, gen)
+    exp_crc = enc[-1].crc                      # the writer's CRCs (crc.New(record).Value())
     from bitalosdb_amd.codec import handles_tensor
     h_t = handles_tensor(h, dev)
     desc = torch.empty(n * 40, dtype=torch.uint8, device=dev)
     voff = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev)
     vals = torch.empty(n * 1024 + 64, dtype=torch.uint8, device=dev)
-    step = lambda: codec.decode_batch(src, src.numel(), h_t, n, 1, out_desc=desc, out_vals=vals, out_val_off=voff)
+    step = lambda: codec.decode_batch(src, src.numel(), h_t, n, 1, expected_crc=exp_crc, out_desc=desc,
+                                      out_vals=vals, out_val_off=voff)
     el, kms = _timed(a, dev, step)
     d = desc.cpu().numpy().view(DESC_DT)
     disk = float(h["length"].astype(np.float64).sum())
     out = {"metric": "GiB/s bithash blocks decoded (device-resident), snappy, 32B key / 1KB value, 1 GPU",
            "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (GPU-encoded snappy tables)",
-           "config": {"workload": "BASELINE configs[2]: 1M snappy blocks, CRC + decompress + decode",
-                      "blocks_per_gpu": n, "mean_record_bytes": round(disk / n, 1),
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (GPU-encoded snappy tables, values: %s)" % gen,
+           "config": {"workload": "BASELINE configs[2]: 1M snappy blocks, CRC-verify (expected_crc = the writer's "
+                                  "CRCs) + decompress + decode",
+                      "values": gen, "blocks_per_gpu": n, "mean_record_bytes": round(disk / n, 1),
+                      "snappy_ratio": round((disk - n * 52.0) / (n * 1024.0), 4),
                       "decoded_GiBps": round(n * 1024 * a.steps / el / 2 ** 30, 3)},
            "status_ok_blocks": int((d["status"] == 0).sum())}
-    # SURVEY 8(d) C3 algorithmic bytes: handle 16 + record L + desc 40 + 1 KiB decoded value per block,
-    # over the whole step (header/CRC pass + scan + snappy kernel; kms = event-timed step)
-    alg = n * (16 + 40 + 1024) + disk
+    out["valid"] = out["status_ok_blocks"] == n
+    # SURVEY 8(d) C3 algorithmic bytes: handle 16 + record L + expected CRC 4 + desc 40 + 1 KiB decoded
+    # value per block, over the whole step (header/CRC pass + scan + snappy kernel; kms = event-timed step)
+    alg = n * (16 + 4 + 40 + 1024) + disk
     out["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                        "traffic": None, "scope": "whole step (k_decode_stream<1> header/CRC pass + size scan + k_snappy_lds + k_snappy_rt)",
                        "step_event_ms": round(kms, 4)}
-    if rank == 0 and world == 1 and not a.no_traffic:
-        out["roofline"].update(traffic_fields(["--config", "c3", "--blocks", str(n)],
-                                              ["k_decode_stream", "k_snappy_lds", "k_snappy_rt"], int(alg),
-                                              "handle 16 + on-disk record + descriptor 40 + 1 KiB value per block"))
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if extras and rank == 0 and world == 1 and not a.no_traffic:
+        out["roofline"].update(traffic_fields(["--config", "c3", "--blocks", str(n), "--values", gen,
+                                               "--no-secondary"],
+                                              ["k_decode_stream", "k_snappy_lds", "k_snappy_rt", "k_chunk_"], int(alg),
+                                              "handle 16 + on-disk record + expected CRC 4 + descriptor 40 + 1 KiB "
+                                              "value per block"))
+    if extras and rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         host = src.cpu().numpy()
         thr = usable_cores()
-        exp, ev, eo = O.decode_batch(host, h, codec=1, nthreads=thr)
+        ecrc = exp_crc.cpu().numpy().view(np.uint32)
+        exp, ev, eo = O.decode_batch(host, h, codec=1, expected_crc=ecrc, nthreads=thr)
         got_v = vals.cpu().numpy()
         par = all(np.array_equal(exp[f], d[f]) for f in d.dtype.names) and \
             got_v[:int(eo[-1])].tobytes() == ev[:int(eo[-1])].tobytes()
         t = time.perf_counter()
         reps = 0
         while time.perf_counter() - t < a.cpu_seconds:
-            O.decode_batch(host, h, codec=1, nthreads=thr, out_val_off=eo)
+            O.decode_batch(host, h, codec=1, expected_crc=ecrc, nthreads=thr, out_val_off=eo)
             reps += 1
         cs = time.perf_counter() - t
         # one thread: the first 100k blocks (a bounded sample), same restated decode
@@ -711,27 +751,40 @@ def run_c3(a, world, rank, local, dev, codec):
         t = time.perf_counter()
         reps1 = 0
         while time.perf_counter() - t < 2.0:
-            O.decode_batch(host, h1, codec=1, nthreads=1, out_val_off=eo[:n1 + 1])
+            O.decode_batch(host, h1, codec=1, expected_crc=ecrc[:n1], nthreads=1, out_val_off=eo[:n1 + 1])
             reps1 += 1
         cs1 = time.perf_counter() - t
         out["cpu_baseline"] = {"value": round(reps * disk / cs / 2 ** 30, 3), "unit": "GiB/s", "cores": thr,
                                "kind": "port", "one_thread": round(reps1 * disk1 / cs1 / 2 ** 30, 3),
-                               "sample": "C restatement (readRecord + CRC + golang/snappy decode), "
+                               "sample": "C restatement (readRecord + CRC verify + golang/snappy decode), "
                                "%d passes over the same %d blocks on %d threads = every core this process may use; "
                                "one_thread: the first %d blocks on 1 thread (%s)" % (reps, n, thr, n1, cpu_info())}
         out["parity_vs_restatement"] = "bit-exact" if par else "MISMATCH"
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+        out["valid"] = bool(out["valid"] and par)
+    return out
 
 
 def run_c4(a, world, rank, local, dev, codec):
-    """BASELINE configs[3]: encode 1M pairs, values U[64, 4096] B -> record-pack + snappy + CRC."""
+    """BASELINE configs[3]: encode 1M pairs, values U[64, 4096] B -> record-pack + snappy + CRC.
+    The line is the --values generator; the other one is nested as a secondary line."""
+    res = c4_measure(a, world, rank, local, dev, codec, a.values, extras=True)
+    if not a.no_secondary:
+        torch.cuda.empty_cache()
+        g2 = _secondary_gen(a.values)
+        sec = c4_measure(a, world, rank, local, dev, codec, g2, extras=False)
+        res["secondary_values_" + g2] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "roofline")}
+        res["secondary_values_" + g2].update(sec["config"])
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def c4_measure(a, world, rank, local, dev, codec, gen, extras):
     from bitalosdb_amd.codec import EncodeBuffers
     n = a.blocks
     g = torch.Generator(device=dev)
     g.manual_seed(synth_seed(rank) + 7)
     val_lens = torch.randint(64, 4097, (n,), generator=g, device=dev, dtype=torch.int64)
-    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, synth_seed(rank))
+    keys, key_off, tr, vals, val_off = _encode_inputs(n, val_lens, dev, synth_seed(rank), gen)
     cap = int(n * 64 + vals.numel() * 7 // 6 + 64)
     out_t = torch.empty(cap, dtype=torch.uint8, device=dev)
     maxt = 4096
@@ -744,9 +797,11 @@ def run_c4(a, world, rank, local, dev, codec):
     res = {"metric": "GiB/s KV input encoded (record-pack + snappy + CRC), values 64B-4KB, 1 GPU",
            "value": round(raw * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic compressible values",
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic compressible values (%s)" % gen,
            "config": {"workload": "BASELINE configs[3]: 1M KV pairs -> record-pack + compress + CRC",
-                      "pairs_per_gpu": n, "input_bytes": int(raw), "output_bytes": total,
+                      "values": gen, "pairs_per_gpu": n, "input_bytes": int(raw), "output_bytes": total,
+                      "snappy_ratio": round((total - n * 52.0) / float(vals.numel()), 4),
                       "tables": int(bufs.summary[1].item())}}
     # SURVEY 8(d) C4 algorithmic bytes: read key 32 + value v + 16 B (offsets, trailer); write the
     # records (52 + c each, = output_bytes) + handle 8 + FNV 4 + CRC 4; whole step (kms = event-timed)
@@ -756,14 +811,16 @@ def run_c4(a, world, rank, local, dev, codec):
                        "scope": "whole step (sizes, scan, k_snappy_enc, split, pack, crc)",
                        "step_event_ms": round(kms, 4),
                        "note": "k_snappy_enc is latency bound (DESIGN.md 4.3); snappy scratch traffic excluded"}
-    if rank == 0 and world == 1 and not a.no_traffic:
-        res["roofline"].update(traffic_fields(["--config", "c4", "--blocks", str(n)],
+    if extras and rank == 0 and world == 1 and not a.no_traffic:
+        res["roofline"].update(traffic_fields(["--config", "c4", "--blocks", str(n), "--values", gen,
+                                               "--no-secondary"],
                                               ["k_enc_sizes", "k_snappy_enc", "k_enc_split", "k_enc_tsize",
-                                               "k_enc_pack", "k_enc_crc"], int(alg),
+                                               "k_enc_pack", "k_enc_crc", "k_enc_class", "k_snappy_maxlen",
+                                               "k_chunk_"], int(alg),
                                               "key + value + 16 B in, records + handle/FNV/CRC out per pair; the "
                                               "snappy scratch written by k_snappy_enc and read by k_enc_pack is "
                                               "extra traffic"))
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if extras and rank == 0 and world == 1 and not a.no_cpu:
         from oracle import oracle as O
         vo = val_off.cpu().numpy().astype(np.uint64)
         vb = vals.cpu().numpy()
@@ -799,8 +856,7 @@ def run_c4(a, world, rank, local, dev, codec):
                                          "core, one writer per contiguous pair range; one_thread: the first %d "
                                          "pairs on 1 thread (%s)" % (n, reps, cs, thr, m1, cpu_info())}
         res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
-    if rank == 0:
-        print(json.dumps(res), flush=True)
+    return res
 
 
 C5_RECORDS_PER_TABLE = 124_738      # 128 MiB / 1076 B, the add that crosses the limit included
@@ -828,7 +884,7 @@ def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
     snappy = codec_name == "snappy"
     t_build = time.perf_counter()
     if snappy:
-        src_t, h, exp_crc, raw = synth.table_set_snappy(codec, owned, R, device=dev, seed=synth.SEED)
+        src_t, h, exp_crc, raw = synth.table_set_snappy(codec, owned, R, device=dev, seed=synth.SEED, gen=a.values)
     else:
         src_t, h, meta = synth.table_set(owned, R, device=dev, seed=synth.SEED, first_file_num=1)
         raw = len(h) * 1024
@@ -907,6 +963,9 @@ def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
     }
     if snappy:
         out["decoded_GiBps"] = round(raw_total * a.steps / el_max / 2 ** 30, 3)
+        out["config"]["values"] = a.values
+    if world > 1:
+        out.update(shard.scaling_fields(elapsed, achieved / HBM_PEAK_GBPS, dev))
     if rank == 0 and world == 1 and with_cpu and not a.no_cpu and n:
         from oracle import oracle as O
         # parity + baseline on a bounded sample: the first table (the restatement decodes it bit for bit)

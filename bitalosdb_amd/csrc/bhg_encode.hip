@@ -156,7 +156,8 @@ __device__ __forceinline__ uint32_t table_of(const uint32_t *ts, uint32_t nt, ui
 //  phase B, wave per record: the value from qa on in 16-B output chunks (4-aligned dwordx4
 //    stores), each from a 20-B aligned source window and a byte funnel; two records per pass
 //    with all loads issued before the first store.
-// A record with a ukey > 36 B is packed byte by byte by its lane (rare; slow but exact).
+// A record with a ukey > 36 B has its prefix (header | ukey | trailer | value bytes up to qa)
+// written byte by byte by its lane (rare); its value still goes through phase B.
 // (The wave-per-record version loaded the metadata record by record: ~6 dependent memory round
 // trips per record, 1.42 ms per C4 batch; the dword version of this one 1.05 ms.)
 __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
@@ -230,8 +231,9 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                         if (q + b >= dst && q + b < dend) gst<uint8_t>(q + b, (uint8_t)(x >> (8 * b)));
                 }
             }
-        } else if (ok) {  // ukey > 36 B: the whole record byte by byte
-            for (uint32_t o = 0; o < L; o++) {
+        } else if (ok) {  // ukey > 36 B: the prefix [dst, qa) byte by byte; phase B copies the value from qa
+            const uint32_t np = (uint32_t)((qa < dend ? qa : dend) - dst);
+            for (uint32_t o = 0; o < np; o++) {
                 uint32_t by;
                 if (o < 12) by = ((o < 4 ? kl + 8 : o < 8 ? vl : fn) >> (8 * (o & 3))) & 0xffu;
                 else if (o < 12 + kl) by = gld<uint8_t>(kp + (o - 12));
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
             }
         }
         // ---------------- phase B: wave per record, the value from qa on
-        uint64_t todo = __ballot(ok && shortk && qa < dend);
+        uint64_t todo = __ballot(ok && qa < dend);
         while (todo) {
             int jr[2];
             jr[0] = __builtin_ctzll(todo);
@@ -411,7 +413,9 @@ __global__ __launch_bounds__(256) void k_repack_prep(const uint8_t *src, uint64_
             k = ldu32(p, end);
             v = ldu32(p + 4, end);
             fn = ldu32(p + 8, end);
-            if (k >= 1 && 12ull + k + v == r.length) {
+            // readRecord's nil rules (block2.go:57-66): ikeySize == 0 or valueSize == 0 is no record
+            // (TableIterator.findEntry stops at valueSize <= 0, table.go:373)
+            if (k >= 1 && v >= 1 && 12ull + k + v == r.length) {
                 st = BHG_ST_OK;
                 kl = k >= 8 ? k - 8 : 0u;
                 tr = k >= 8 ? ldu64(p + 12 + k - 8, end) : 255ull;  // InternalKeyKindInvalid

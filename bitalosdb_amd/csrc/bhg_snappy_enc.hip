@@ -574,7 +574,8 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
-    uint16_t *gt = gtables + (size_t)gw * 16384;
+    // the small-value launch passes no gtables: its blocks (<= SE_CAP_SMALL) always fit CAP
+    uint16_t *gt = gtables != nullptr ? gtables + (size_t)gw * 16384 : nullptr;
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef BHG_SE_PROF
     const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
@@ -811,8 +812,12 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
     hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
                        cnt);
     if (hipError_t e = hipGetLastError()) return e;
+    // the small-value class never reaches se_block_serial (its values, hence its blocks, are
+    // <= SE_CAP_SMALL = its LDS capacity), so it gets no global hash tables: gtables is sized for
+    // the large-value grid only (snappy_enc_grid)
+    static_assert(SE_CAP_SMALL <= SE_CAP, "small-value class must fit the LDS block");
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>), dim3(enc_grid<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
-                       val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen, gtables);
+                       val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen, nullptr);
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG, 3>), dim3(enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n)), dim3(64 * BHG_SE_WPG), 0,
                        L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * BHG_SE_HEADS, scratch, scap, soff, clen,

@@ -21,6 +21,7 @@
 //   k_tail_heads   lane/position: run-head flags -> scan -> run index
 //   k_tail_runs    lane/run: run position, key, length, conflict flag
 //   k_tail_keep    lane/position: last occurrence of its key in a conflict run
+//   k_tail_klist   scan of keep -> compacted kept positions
 //   k_tail_dedupe  lane/kept position: a key kept by two runs of one table
 //                  (the caller passed one key under two khash values) stays
 //                  only where conflictKeys[key] was assigned last
@@ -70,6 +71,8 @@ struct TailArgs {
     uint64_t *run_key;              // n
     uint8_t *run_conf;              // n
     uint64_t *keep, *kpos;          // n+1
+    uint64_t *kscan;                // n+1: exclusive scan of keep
+    uint32_t *klist;                // n: kept positions, in sorted order
     uint32_t *kat;                  // n: when updateHash last assigned conflictKeys[key] from this run
     uint32_t *clist, *cord;         // n
     uint64_t *csz;                  // n+1: conflict entry sizes -> offsets
@@ -240,21 +243,32 @@ __global__ __launch_bounds__(256) void k_tail_keep(TailArgs a) {
     }
 }
 
+// kept positions, compacted: klist[kscan[j]] = j (kscan = exclusive scan of keep)
+__global__ __launch_bounds__(256) void k_tail_klist(TailArgs a) {
+    GRID_LOOP(j, a.n) {
+        if (a.kscan[j + 1] != a.kscan[j]) a.klist[a.kscan[j]] = (uint32_t)j;
+    }
+}
+
 // conflictKeys is one map per table, keyed by user key: a key kept by two runs (two khash
 // values for one key, possible through AddIkey) keeps the run that assigned it last.  Without
-// this the conflict list would hold a key twice and the rank permutation would break.
+// this the conflict list would hold a key twice and the rank permutation would break.  Each
+// kept position compares itself with the kept positions of its own table only (klist, sorted
+// by table like sk_s): O(kept_t^2) per table, not O(kept_t x records_t).
 __global__ __launch_bounds__(256) void k_tail_dedupe(TailArgs a) {
+    const uint32_t K = (uint32_t)a.kscan[a.n];
     GRID_LOOP(j, a.n) {
         uint64_t f = a.keep[j];
         if (f) {
             const uint64_t t = a.sk_s[j] >> 32;
-            const uint32_t p0 = lower_bound(0, a.n, t << 32, [&](uint32_t q) { return a.sk_s[q]; });
-            const uint32_t p1 = lower_bound(p0, a.n, (t + 1) << 32, [&](uint32_t q) { return a.sk_s[q]; });
+            const uint32_t g0 = lower_bound(0, K, t << 32, [&](uint32_t g) { return a.sk_s[a.klist[g]]; });
+            const uint32_t g1 = lower_bound(g0, K, (t + 1) << 32, [&](uint32_t g) { return a.sk_s[a.klist[g]]; });
             uint64_t kp; uint32_t kl;
             rec_key(a, a.idx_s[j], kp, kl);
             const uint32_t at = a.kat[j];
-            for (uint32_t q = p0; q < p1 && f; q++) {
-                if (q == j || !a.keep[q] || a.kat[q] < at || (a.kat[q] == at && q < j)) continue;
+            for (uint32_t g = g0; g < g1 && f; g++) {
+                const uint32_t q = a.klist[g];
+                if (q == j || a.kat[q] < at || (a.kat[q] == at && q < j)) continue;
                 uint64_t kq; uint32_t lq;
                 rec_key(a, a.idx_s[q], kq, lq);
                 if (key_eq(kp, kl, kq, lq)) f = 0;
@@ -532,7 +546,7 @@ size_t tail_scratch_bytes(uint32_t n, uint32_t ntables) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t N = (size_t)n + 1, T = (size_t)ntables + 1;
     return al(sort_tmp) + 2 * al(N * 8) + 2 * al(N * 4) + 2 * al(N * 8) + 2 * al(N * 4) + al(N * 8) + al(N) +
-           2 * al(N * 8) + al(N * 4) + 2 * al(N * 4) + al(N * 8) + 2 * al(T * 4) + al(T * 8) + al(T * 8) +
+           3 * al(N * 8) + 2 * al(N * 4) + 2 * al(N * 4) + al(N * 8) + 2 * al(T * 4) + al(T * 8) + al(T * 8) +
            al(T * 16) + al(T * 4) + al(scan_scratch_bytes(N > T ? N : T)) + 24 * 256;
 }
 
@@ -555,6 +569,7 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     a.run_pos = (uint32_t *)take(N * 4); a.run_len = (uint32_t *)take(N * 4);
     a.run_key = (uint64_t *)take(N * 8); a.run_conf = take(N);
     a.keep = (uint64_t *)take(N * 8); a.kpos = (uint64_t *)take(N * 8); a.kat = (uint32_t *)take(N * 4);
+    a.kscan = (uint64_t *)take(N * 8); a.klist = (uint32_t *)take(N * 4);
     a.clist = (uint32_t *)take(N * 4); a.cord = (uint32_t *)take(N * 4);
     a.csz = (uint64_t *)take(N * 8);
     a.tab_run = (uint32_t *)take(TT * 4); a.tab_c = (uint32_t *)take(TT * 4);
@@ -572,6 +587,8 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     if ((e = launch_exclusive_scan_u64(L, a.head, a.runidx, n, scan_s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_runs, dim3(g), dim3(256), 0, L.stream, a);
     hipLaunchKernelGGL(k_tail_keep, dim3(g), dim3(256), 0, L.stream, a);
+    if ((e = launch_exclusive_scan_u64(L, a.keep, a.kscan, n, scan_s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tail_klist, dim3(g), dim3(256), 0, L.stream, a);
     hipLaunchKernelGGL(k_tail_dedupe, dim3(g), dim3(256), 0, L.stream, a);
     if ((e = launch_exclusive_scan_u64(L, a.kpos, a.kpos, n, scan_s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_clist, dim3(g), dim3(256), 0, L.stream, a);

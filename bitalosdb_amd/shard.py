@@ -52,3 +52,31 @@ def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
     c = c.cpu().tolist()
     return float(t.item()), int(c[0]), int(c[1]), (int(c[2]) & 0xFFFFFFFF) | ((int(c[3]) & 0xFFFFFFFF) << 32)
+
+
+def gather_floats(values, device):
+    """Every rank's list of floats (all_gather; gloo through host tensors), rank order."""
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if multi and dist.get_backend() == "gloo":
+        device = "cpu"
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if not multi:
+        return [t.cpu().tolist()]
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
+def scaling_fields(elapsed_s, frac, device):
+    """Fields that make an N > 1 line self-describing: which N = 1 record its
+    speed-up is taken against, every rank's timed elapsed (max / min: the imbalance of the
+    round-robin table split) and every rank's roofline fraction."""
+    g = gather_floats([elapsed_s, frac], device)
+    el = [r[0] for r in g]
+    return {"base_n1": "strong_c5",
+            "speedup_rule": "speed-up at N = this line's value / the N = 1 BENCH line's nested strong_c5.value "
+                            "(the same fixed corpus on one GPU), never / its top-level value (the 1M-block C2 batch)",
+            "rank_elapsed_s": {"max": round(max(el), 6), "min": round(min(el), 6),
+                               "imbalance": round(max(el) / min(el), 4) if min(el) > 0 else None,
+                               "per_rank": [round(x, 6) for x in el]},
+            "per_gpu_frac": [round(r[1], 4) for r in g]}

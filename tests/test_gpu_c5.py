@@ -117,7 +117,7 @@ def test_c5_snappy_one_launch(codec):
         assert int(voff[-1]) == raw and (np.diff(voff) == 1024).all()
         # every decoded value is the generator's input (regenerated per table on the GPU)
         for t in range(T):
-            want = synth.compressible_values_gpu(R, 1024, device=dev, seed=synth.table_seed(synth.SEED, t) + 1)
+            want = synth.values_gpu("dict", R, 1024, device=dev, seed=synth.table_seed(synth.SEED, t) + 1)
             got = vals_t[t * R * 1024:(t + 1) * R * 1024].view(R, 1024)
             assert torch.equal(got, want), t
         whole = _digest(d)

@@ -113,22 +113,26 @@ def test_compaction_repack_pipeline(codec, compressor, init):
 
 
 def test_repack_bad_handles(codec):
-    """Handles that are not whole records -> RECORD_NIL, nothing written for them."""
+    """Handles that are not whole records -> RECORD_NIL, nothing written for them;
+    a whole record with valueSize 0 is RECORD_NIL too (readRecord's nil rule,
+    block2.go:60; TableIterator.findEntry stops there, table.go:373)."""
+    import struct
     from bitalosdb_amd.codec import as_device_bytes, handles_tensor
     recs = [O.record_set(b"key%d" % i, (i + 1) << 8 | 1, b"v" * (10 + i), 7) for i in range(6)]
+    recs.append(struct.pack("<III", 12, 0, 7) + b"kkkk" + struct.pack("<Q", 9 << 8 | 1))   # valueSize 0
     src = b"".join(recs)
     offs = np.cumsum([0] + [len(r) for r in recs])
-    hs = [(int(offs[i]), len(recs[i]), 0) for i in range(6)]
+    hs = [(int(offs[i]), len(recs[i]), 0) for i in range(len(recs))]
     hs[1] = (hs[1][0], hs[1][1] - 1, 0)              # length mismatch
     hs[3] = (len(src) - 5, 30, 0)                    # past the end
     h = np.array(hs, dtype=O.HANDLE_DT)
     with torch.cuda.stream(codec.stream):
         src_t = as_device_bytes(src, codec.device)
         ht = handles_tensor(h, codec.device)
-        out_t, bufs = codec.repack_batch(src_t, ht, 6)
+        out_t, bufs = codec.repack_batch(src_t, ht, len(recs))
         codec.sync()
     st = bufs.status.cpu().numpy().view(np.uint32)
-    assert list(st) == [0, O.RECORD_NIL, 0, O.RECORD_NIL, 0, 0]
+    assert list(st) == [0, O.RECORD_NIL, 0, O.RECORD_NIL, 0, 0, O.RECORD_NIL]
     size = int(bufs.table_size[0].item())
     assert out_t[:size].cpu().numpy().tobytes() == recs[0] + recs[2] + recs[4] + recs[5]
 

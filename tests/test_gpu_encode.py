@@ -62,6 +62,22 @@ def test_encode_k1_split_sizes(codec):
     assert sizes == [1049651, 1049767, 405072]
 
 
+@pytest.mark.parametrize("compressor", [0, 1])
+def test_encode_long_keys_big_values(codec, compressor):
+    """User keys of 37..64 B (past the pack kernel's 36-B register prefix) with
+    values of several KiB: the lane writes the prefix, the wave copies the value
+    (phase B) -- byte-exact with the restated writer at every alignment."""
+    rng = random.Random(40 + compressor)
+    n = 400
+    keys = [rb(rng, rng.choice([37, 40, 41, 48, 63, 64])) for _ in range(n)]
+    vals = [compressible(rng, rng.choice([1, 5, 3000, 4096, 9001, 20000])) if i % 2 else
+            rb(rng, rng.choice([2, 700, 5000, 16384])) for i in range(n)]
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    got = codec.encode(keys, tr, vals, compressor=compressor, file_nums=list(range(1, 20)), table_max=1 << 20)
+    exp = O.encode_batch(keys, tr, vals, codec=compressor, file_nums=list(range(1, 20)), table_max=1 << 20)
+    check(got, exp)
+
+
 def test_encode_too_large(codec):
     rng = random.Random(8)
     keys = [b"a" * 10, b"b" * ((33 << 10) - 7), b"c" * 5, b"d" * ((33 << 10) - 8)]

@@ -1,10 +1,10 @@
 """Full-size GPU parity for BASELINE configs[2] and configs[3] (the C2 batch
 is in test_gpu_decode.py::test_full_size_c2_parity):
 
-* C3: 1M snappy blocks (32 B key / 1 KiB value, the SURVEY §8d compressible
-  generator, GPU-encoded into 128 MiB tables): every descriptor and every
+* C3: 1M snappy blocks (32 B key / 1 KiB value, the SURVEY §8d dictionary
+  generator and the 16-B-chunk generator, GPU-encoded into 128 MiB tables): every descriptor and every
   decoded byte against the restatement, and every value against its input;
-* C4: 1M pairs with values U[64, 4096] B through bhg_encode_batch (snappy,
+* C4: 1M pairs with values U[64, 4096] B (both generators) through bhg_encode_batch (snappy,
   TableMaxSize 128 MiB): records, positions, handles, tables, FNV-1, CRCs and
   statuses against the restated BithashWriter.Add sequence -- every split
   boundary, u64 positions past 1 GiB and the scan over 489+ chunks included."""
@@ -25,12 +25,12 @@ def codec():
     c.close()
 
 
-def _encode(codec, n, val_lens, seed, compressor):
+def _encode(codec, n, val_lens, seed, compressor, gen="dict"):
     from bitalosdb_amd import synth
     from bitalosdb_amd.codec import EncodeBuffers
     dev = codec.device
     with torch.cuda.stream(codec.stream):
-        keys, key_off, tr, vals, val_off = synth.kv_pairs_gpu(n, val_lens, device=dev, seed=seed)
+        keys, key_off, tr, vals, val_off = synth.kv_pairs_gpu(n, val_lens, device=dev, seed=seed, gen=gen)
         out = torch.empty(int(n * 64 + vals.numel() * 7 // 6 + 64), dtype=torch.uint8, device=dev)
         maxt = 256
         fns = torch.arange(1, maxt + 1, dtype=torch.int32, device=dev)
@@ -41,11 +41,12 @@ def _encode(codec, n, val_lens, seed, compressor):
     return (keys, key_off, tr, vals, val_off), out, bufs
 
 
-def test_full_size_c3_parity(codec):
+@pytest.mark.parametrize("gen", ["dict", "chunk16"])
+def test_full_size_c3_parity(codec, gen):
     from bitalosdb_amd.codec import handles_tensor
     n = 1_000_000
     val_lens = torch.full((n,), 1024, dtype=torch.int64)
-    (keys, _, _, vals, _), out, bufs = _encode(codec, n, val_lens, 0xC3, 1)
+    (keys, _, _, vals, _), out, bufs = _encode(codec, n, val_lens, 0xC3, 1, gen)
     total = int(bufs.summary[0].item())
     assert int(bufs.summary[2].item()) == 0 and total > 1 << 29
     h = np.zeros(n, dtype=O.HANDLE_DT)
@@ -77,11 +78,12 @@ def test_full_size_c3_parity(codec):
     assert gv.tobytes() == vals.cpu().numpy().tobytes()          # round trip to the encoder's input
 
 
-def test_full_size_c4_parity(codec):
+@pytest.mark.parametrize("gen", ["dict", "chunk16"])
+def test_full_size_c4_parity(codec, gen):
     n = 1_000_000
     g = torch.Generator().manual_seed(0xC4)
     val_lens = torch.randint(64, 4097, (n,), generator=g, dtype=torch.int64)
-    (keys, key_off, tr, vals, val_off), out, bufs = _encode(codec, n, val_lens, 0xC4, 1)
+    (keys, key_off, tr, vals, val_off), out, bufs = _encode(codec, n, val_lens, 0xC4, 1, gen)
     nt = int(bufs.summary[1].item())
     assert nt >= 8
     kb = keys.cpu().numpy().tobytes()

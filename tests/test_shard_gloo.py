@@ -132,7 +132,13 @@ def test_bench_self_spawn_world2():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
+    sf = d.pop("scaling_fields")
     assert d == {"config": "spawncheck", "n_gpus": 2, "ranks_seen": 2, "rank_sum": 1, "spawned": True}
+    # the N > 1 line's self-describing fields (shard.scaling_fields, shared with c5_measure)
+    assert sf["base_n1"] == "strong_c5" and "strong_c5" in sf["speedup_rule"]
+    assert sf["rank_elapsed_s"]["per_rank"] == [1.0, 1.5]
+    assert sf["rank_elapsed_s"]["max"] == 1.5 and sf["rank_elapsed_s"]["min"] == 1.0
+    assert sf["rank_elapsed_s"]["imbalance"] == 1.5 and sf["per_gpu_frac"] == [0.5, 0.5]
 
 
 def test_bench_gpus_must_match_world_size():
