@@ -815,7 +815,7 @@ def c4_measure(a, world, rank, local, dev, codec, gen, extras):
         res["roofline"].update(traffic_fields(["--config", "c4", "--blocks", str(n), "--values", gen,
                                                "--no-secondary"],
                                               ["k_enc_sizes", "k_snappy_enc", "k_enc_split", "k_enc_tsize",
-                                               "k_enc_pack", "k_enc_crc", "k_enc_class", "k_snappy_maxlen",
+                                               "k_enc_pack", "k_enc_meta", "k_enc_class", "k_snappy_maxlen",
                                                "k_chunk_"], int(alg),
                                               "key + value + 16 B in, records + handle/FNV/CRC out per pair; the "
                                               "snappy scratch written by k_snappy_enc and read by k_enc_pack is "

@@ -31,6 +31,7 @@ struct bhg_ctx {
     void *h_vals = nullptr; size_t h_vals_cap = 0;
     uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
     uint32_t *stab = nullptr;  // stream-kernel shift tables (bhg_decode_stream.h build_stream_tab)
+    uint32_t *xtab = nullptr;  // CrcR8-kernel shift tables (bhg_crc_tables.h build_xtab)
     // pipelined host path: kPipe slots, each with its own stream and device ring buffers
     static constexpr int kPipe = 3;
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
@@ -65,6 +66,7 @@ bhg::Launch launch_of(bhg_ctx *c, void *stream) {
     L.num_cus = c->num_cus;
     L.ztab = c->ztab;
     L.stab = c->stab;
+    L.xtab = c->xtab;
     return L;
 }
 
@@ -173,6 +175,12 @@ bhg_ctx *bhg_create(int device, int flags) {
         ok = hipMalloc(reinterpret_cast<void **>(&c->stab), z.size() * 4) == hipSuccess &&
              hipMemcpy(c->stab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
+    if (ok) {
+        std::vector<uint32_t> z(1024u * bhg::XTAB_N);
+        bhg::build_xtab(z.data());
+        ok = hipMalloc(reinterpret_cast<void **>(&c->xtab), z.size() * 4) == hipSuccess &&
+             hipMemcpy(c->xtab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
     if (!ok) {
         bhg_destroy(c);
         return nullptr;
@@ -193,6 +201,7 @@ void bhg_destroy(bhg_ctx *c) {
     if (c->h_vals) (void)hipFree(c->h_vals);
     if (c->ztab) (void)hipFree(c->ztab);
     if (c->stab) (void)hipFree(c->stab);
+    if (c->xtab) (void)hipFree(c->xtab);
     if (c->pool) {
         (void)hipDeviceSynchronize();  // frees enqueued on caller streams have completed
         (void)hipMemPoolDestroy(c->pool);

@@ -171,6 +171,83 @@ struct Crc4Lds {
     }
 };
 
+// LDS by byte address: kernels that keep all their LDS in one __shared__ array (so that hipcc sees
+// a single object) address tables and staging areas as byte offsets into it.
+template <class T>
+__device__ __forceinline__ uint32_t lds_addr(T *p) {
+    return (uint32_t)(size_t)(__attribute__((address_space(3))) T *)p;
+}
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((size_t)a);
+}
+template <class V>
+__device__ __forceinline__ void lds_st(uint32_t a, V v) {
+    *reinterpret_cast<__attribute__((address_space(3))) V *>((size_t)a) = v;
+}
+
+// Slice-by-4 tables T0..T3 with 8 replicas in 32 KiB of LDS: byte address (b << 7) | (k << 5) |
+// (r << 2) for T_k[b], replica r.  Lane l reads replica l % 8, and the four lane octets of a 32-lane
+// half take the four tables in rotated order (octet g's i-th lookup of a word is table (i + g) % 4),
+// so one ds_read_b32 of a half touches banks (k << 3) | r -- 32 different banks for any data:
+// conflict free like Crc4Perm at a quarter of its LDS.  One word = 4 x (bfe + shift-add + ds_read)
+// + xors.
+struct CrcR8 {
+    static constexpr uint32_t kBytes = 32768;
+    uint32_t tb;     // LDS byte address of the tables
+    uint32_t sh[4];  // byte position of x that lookup i takes (8 * (3 - k))
+    uint32_t ko[4];  // tb + table / replica offset of lookup i
+    __device__ __forceinline__ explicit CrcR8(uint32_t tbase) : tb(tbase) {
+        const uint32_t lane = threadIdx.x & 63, r = lane & 7, g = (lane >> 3) & 3;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t k = (i + g) & 3;
+            sh[i] = 8 * (3 - k);
+            ko[i] = tbase + ((k << 5) | (r << 2));
+        }
+    }
+    __device__ __forceinline__ uint32_t look(uint32_t x, int i) const {
+        return lds_ld32((__builtin_amdgcn_ubfe(x, sh[i], 8) << 7) + ko[i]);
+    }
+    // absorb one little-endian word (Go's crc32 slicing-by-4 step): c' = T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]
+    __device__ __forceinline__ uint32_t word(uint32_t c, uint32_t w) const {
+        const uint32_t x = c ^ w;
+        return look(x, 0) ^ look(x, 1) ^ look(x, 2) ^ look(x, 3);
+    }
+    __device__ __forceinline__ uint32_t step(uint32_t c) const {  // one byte through T0 (k = 0)
+        return (c >> 8) ^ lds_ld32(((c & 0xffu) << 7) + tb + ((threadIdx.x & 7u) << 2));
+    }
+    // absorb the low nb (0..4) bytes of x
+    __device__ __forceinline__ uint32_t partial(uint32_t c, uint32_t x, uint32_t nb) const {
+        if (nb >= 4) return word(c, x);
+        c ^= x & ((1u << (8 * nb)) - 1u);
+#pragma unroll
+        for (uint32_t s = 0; s < 3; s++) {
+            const uint32_t nx = step(c);
+            c = s < nb ? nx : c;
+        }
+        return c;
+    }
+    // fill the 32 KiB at tbase (whole workgroup)
+    static __device__ __forceinline__ void fill(uint32_t tbase) {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x) {
+            const uint32_t k = t >> 8, b = t & 255;
+            uint32_t v = crc_table_entry(b);
+            for (uint32_t q = 0; q < k; q++) v = (v >> 8) ^ crc_table_entry(v & 0xffu);
+            const uint32_t a = tbase + ((b << 7) | (k << 5));
+            lds_st(a, v4{v, v, v, v});
+            lds_st(a + 16, v4{v, v, v, v});
+        }
+    }
+};
+
+// Z_n(c) from an LDS shift table at byte address zt (4 x 256 words, S[k][i] = Z_n(i << 8k),
+// bhg_crc_tables.h): the CRC state after n more zero bytes
+__device__ __forceinline__ uint32_t zshift(uint32_t zt, uint32_t c) {
+    return lds_ld32(zt + ((c & 0xffu) << 2)) ^ lds_ld32(zt + 1024 + (((c >> 8) & 0xffu) << 2)) ^
+           lds_ld32(zt + 2048 + (((c >> 16) & 0xffu) << 2)) ^ lds_ld32(zt + 3072 + ((c >> 24) << 2));
+}
+
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) {  // crc.go:31-33
     return ((c >> 15) | (c << 17)) + 0xa282ead8u;
 }

@@ -7,13 +7,15 @@
 //   k_enc_split   one workgroup: table split points -- after each successful
 //                 add, meta.Size >= TableMaxSize starts the next table
 //                 (bithash_writer.go:38,47-67); a 1024-ary search per table
-//   k_enc_pack    one WAVE per record: coalesced dword stores of
-//                 header | ukey | trailer | value into the output stream
-//   k_enc_crc     one LANE per record: masked CRC-32C of the packed record
-//                 (line-aligned windows, slice-by-4 LDS tables) + FNV-1 of
-//                 the user key (writer.go:246) + handle / table outputs
+//   k_enc_pack    wave per tile of 64 records: header | ukey | trailer |
+//                 value into the output stream, FNV-1 of the user key
+//                 (writer.go:246) and the masked CRC-32C of each record
+//                 computed from the registers the bytes are stored from (the
+//                 packed output is not read back)
+//   k_enc_meta    lane per record: handle / table / status outputs
 // value' is the raw value (NoCompressor) or its golang/snappy encoding
 // (bhg_snappy_enc.hip) staged in ctx scratch.
+#include "bhg_crc_tables.h"
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -44,6 +46,7 @@ struct EncArgs {
     uint8_t *out;
     uint64_t out_cap;
     uint64_t *lens;               // scratch: L per record, then exclusive scan -> positions (n+1)
+    const uint32_t *xtab;         // the context's CrcR8 shift tables (bhg_crc_tables.h build_xtab)
     bhg_encode_out o;
 };
 
@@ -145,26 +148,48 @@ __device__ __forceinline__ uint32_t table_of(const uint32_t *ts, uint32_t nt, ui
     return lo;
 }
 
-#define ENC_WAVES 4
+#define ENC_WAVES 8
 #define ENC_PACK_K 2  // 16-B value chunks per lane per record pass (2 KiB)
+// LDS of the pack kernel: CrcR8 (32 KiB) + Z_16 .. Z_1024 (7 x 4 KiB) = 60 KiB, two workgroups per CU
+constexpr uint32_t kPackZ = 7;
+constexpr uint32_t kPackLds = CrcR8::kBytes + kPackZ * 4096;
 // One WAVE per tile of 64 records (records are back to back in `out`).
-//  phase A, lane = record: metadata, then the record's prefix (header | ukey | trailer, <= 56 B
-//    for ukeys <= 36 B) and the value bytes up to the next 4-aligned output address qa,
-//    assembled byte by byte from registers (header, trailer) and dword windows of the key and
-//    the value head, and written as dwords (the first one, shared with the previous record, as
-//    bytes).  Per-byte work is spread over 64 records per instruction.
+//  phase A, lane = record: metadata, FNV-1 of the user key, then the record's prefix (header |
+//    ukey | trailer, <= 56 B for ukeys <= 36 B) and the value bytes up to the next 4-aligned
+//    output address qa, assembled byte by byte from registers (header, trailer) and dword
+//    windows of the key and the value head, and written as dwords (the first one, shared with
+//    the previous record, as bytes).  Per-byte work is spread over 64 records per instruction.
+//    The lane also runs the record's CRC over these dwords: P = crc_0 of the prefix with crc.New's
+//    ~0 start folded into the record's first 4 bytes (crc_~0(X) = crc_0(X ^ ~0 at bytes 0..3);
+//    the bytes before the record in the first dword are 0, and leading zeros leave crc_0 at 0).
 //  phase B, wave per record: the value from qa on in 16-B output chunks (4-aligned dwordx4
 //    stores), each from a 20-B aligned source window and a byte funnel; two records per pass
-//    with all loads issued before the first store.
+//    with all loads issued before the first store.  Chunk c (0 .. nc-1) sits on lane c % 64;
+//    each lane Horner-folds the crc_0 of its full chunks (stride 64 chunks: Z_1024), lane 63
+//    starting from P (the prefix ends at qa: it is chunk -1), then
+//        S = sum_lanes Z_{16 d}(acc),  d = (nc - 2 - lane) mod 64 (chunks after the lane's last)
+//    (six conditional shifts, a wave xor-reduce), and the lane holding the last chunk (1..16
+//    bytes) absorbs it into S: the record's CRC state.  CRC linearity over GF(2):
+//    crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B).
 // A record with a ukey > 36 B has its prefix (header | ukey | trailer | value bytes up to qa)
-// written byte by byte by its lane (rare); its value still goes through phase B.
+// written byte by byte by its lane (rare), P bytewise; its value still goes through phase B.
 // (The wave-per-record version loaded the metadata record by record: ~6 dependent memory round
-// trips per record, 1.42 ms per C4 batch; the dword version of this one 1.05 ms.)
+// trips per record, 1.42 ms per C4 batch; the dword version of this one 1.05 ms.  The CRC used to
+// be a separate lane-per-record kernel that read the 1 GB of packed records back: 0.46 ms and
+// 1.27 GB of a C4 step.)
 __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    if (ntab == 0) return;  // split failed (max_tables too small): every thread leaves
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[kPackLds / 4];
+    const uint32_t tb = lds_addr(lds_all), zb = tb + CrcR8::kBytes;
+    CrcR8::fill(tb);
+    for (uint32_t t = threadIdx.x; t < kPackZ * 1024; t += blockDim.x)
+        lds_all[CrcR8::kBytes / 4 + t] = a.xtab[XZ16 * 1024 + t];
+    __syncthreads();
+    const CrcR8 crc(tb);
+    const uint32_t Z1024 = zb + 4096 * (XZ1024 - XZ16);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = gridDim.x * ENC_WAVES;
-    const uint32_t ntab = (uint32_t)a.o.summary[1];
-    if (ntab == 0) return;  // split failed (max_tables too small)
     const uint32_t ntiles = (a.n + 63) / 64;
     const uint64_t dummy = (uint64_t)a.lens;  // a valid, 16-B aligned address for loads whose result is unused
     for (uint32_t tile = blockIdx.x * ENC_WAVES + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
@@ -192,12 +217,37 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
         // key window: 10 dwords from ka (ukey <= 36 B at any alignment); value head: 2 dwords from va
         uint32_t kw[10], vw[2];
         const uint64_t ka = kp & ~3ull, va = vp & ~3ull, kend = kp + kl, vend = vp + vl;
+        const bool kload = r < a.n && shortk && (ok || a.khash == nullptr);
 #pragma unroll
-        for (int u = 0; u < 10; u++) kw[u] = gld<uint32_t>(ok && shortk && ka + 4 * u < kend ? ka + 4 * u : dummy);
+        for (int u = 0; u < 10; u++) kw[u] = gld<uint32_t>(kload && ka + 4 * u < kend ? ka + 4 * u : dummy);
 #pragma unroll
         for (int u = 0; u < 2; u++) vw[u] = gld<uint32_t>(ok && shortk && va + 4 * u < vend ? va + 4 * u : dummy);
+        const uint32_t kd = (uint32_t)(kp - ka);
+        // FNV-1 of the user key (writer.go:246, every record) or the caller's khash (AddIkey, :249)
+        if (r < a.n) {
+            uint32_t fnv;
+            if (a.khash != nullptr) {
+                fnv = a.khash[r];
+            } else if (shortk) {
+                uint32_t hh = BHG_FNV_OFFSET;
+#pragma unroll
+                for (uint32_t u = 0; u < 9; u++) {
+                    const uint32_t kwd = __builtin_amdgcn_alignbyte(kw[u + 1], kw[u], kd);
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++) {
+                        const uint32_t h2 = (hh * BHG_FNV_PRIME) ^ ((kwd >> (8 * b)) & 0xffu);
+                        hh = 4 * u + b < kl ? h2 : hh;
+                    }
+                }
+                fnv = hh;
+            } else {
+                fnv = fnv1_range(kp, kl, kp + kl);
+            }
+            a.o.fnv1[r] = fnv;
+        }
+        uint32_t pc = 0;  // CRC of the record bytes in [dst, min(qa, dend)), ~0 start folded in
         if (ok && shortk) {
-            const uint32_t kd = (uint32_t)(kp - ka), vd = (uint32_t)(vp - va);
+            const uint32_t vd = (uint32_t)(vp - va);
             const uint32_t nq = (uint32_t)((qa - q0) >> 2);  // <= 16
             for (uint32_t u = 0; u < nq; u++) {
                 uint32_t x = 0;
@@ -230,9 +280,15 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                     for (uint32_t b = 0; b < 4; b++)
                         if (q + b >= dst && q + b < dend) gst<uint8_t>(q + b, (uint8_t)(x >> (8 * b)));
                 }
+                // record bytes 0..3 lie in dwords 0 and 1: u == 0 holds offsets 0 .. 3 - sh at bytes
+                // sh..3, u == 1 offsets 4 - sh .. 3 at bytes 0 .. sh - 1
+                const uint32_t init = u == 0 ? (0xffffffffu << (8 * sh)) : u == 1 ? ((1u << (8 * sh)) - 1u) : 0u;
+                if (q + 4 <= dend) pc = crc.word(pc, x ^ init);
+                else if (q < dend) pc = crc.partial(pc, x ^ init, (uint32_t)(dend - q));
             }
         } else if (ok) {  // ukey > 36 B: the prefix [dst, qa) byte by byte; phase B copies the value from qa
             const uint32_t np = (uint32_t)((qa < dend ? qa : dend) - dst);
+            pc = 0xffffffffu;  // crc.New: bytewise from ~0 (the same state as the folded start)
             for (uint32_t o = 0; o < np; o++) {
                 uint32_t by;
                 if (o < 12) by = ((o < 4 ? kl + 8 : o < 8 ? vl : fn) >> (8 * (o & 3))) & 0xffu;
@@ -240,8 +296,10 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                 else if (o < pre) by = (uint32_t)(tr >> (8 * (o - 12 - kl))) & 0xffu;
                 else by = gld<uint8_t>(vp + (o - pre));
                 gst<uint8_t>(dst + o, (uint8_t)by);
+                pc = crc.step(pc ^ by);
             }
         }
+        if (ok && qa >= dend) a.o.crc[r] = crc_mask(~pc);  // the whole record was in the prefix dwords
         // ---------------- phase B: wave per record, the value from qa on
         uint64_t todo = __ballot(ok && qa < dend);
         while (todo) {
@@ -251,7 +309,7 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
             jr[1] = todo ? __builtin_ctzll(todo) : -1;
             if (todo) todo &= todo - 1;
             uint64_t qb[2], de[2], sb[2], ve[2];
-            uint32_t nc[2];
+            uint32_t nc[2], acc[2], lw[2][4], rl[2];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int j = jr[h] < 0 ? jr[0] : jr[h];
@@ -261,6 +319,10 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                 sb[h] = readlane_u64(vp, j) + (qb[h] - readlane_u64(vdst, j));
                 ve[h] = readlane_u64(vend, j);
                 nc[h] = jr[h] < 0 ? 0u : (uint32_t)((de[h] - qb[h] + 15) >> 4);
+                const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pc, j);
+                acc[h] = lane == 63 ? pj : 0u;  // the prefix is chunk -1: lane 63's first Horner term
+                lw[h][0] = lw[h][1] = lw[h][2] = lw[h][3] = 0;
+                rl[h] = 0;
             }
             const uint32_t ncmax = nc[0] > nc[1] ? nc[0] : nc[1];
             for (uint32_t cb = 0; cb < ncmax; cb += 64 * ENC_PACK_K) {
@@ -313,26 +375,52 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
                                 }
                             }
                         }
+                        if (c + 1 < nc[h]) {  // a full chunk: into this lane's Horner chain
+                            const uint32_t v = crc.word(crc.word(crc.word(crc.word(0u, y.x), y.y), y.z), y.w);
+                            acc[h] = zshift(Z1024, acc[h]) ^ v;
+                        } else {              // the last chunk (1..16 bytes): absorbed after the lane sum
+                            lw[h][0] = y.x; lw[h][1] = y.y; lw[h][2] = y.z; lw[h][3] = y.w;
+                            rl[h] = (uint32_t)(de[h] - q);
+                        }
                     }
+            }
+            // S = sum over lanes of Z_{16 d}(acc), d = chunks after the lane's last full chunk
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if (jr[h] < 0) continue;
+                const uint32_t d = (uint32_t)((int32_t)nc[h] - 2 - (int32_t)lane) & 63u;
+                uint32_t v = acc[h];
+#pragma unroll
+                for (uint32_t z = 0; z < 6; z++) {
+                    const uint32_t sv = zshift(zb + 4096 * z, v);  // Z_{16 << z}
+                    v = (d >> z) & 1u ? sv : v;
+                }
+#pragma unroll
+                for (int m = 1; m < 64; m <<= 1) v ^= __shfl_xor(v, m, 64);
+                if (lane == ((nc[h] - 1) & 63u)) {
+                    const uint32_t nw = rl[h] >> 2, nb = rl[h] & 3;
+#pragma unroll
+                    for (uint32_t w = 0; w < 4; w++)
+                        if (w < nw) v = crc.word(v, lw[h][w]);
+                    if (nb) {
+                        uint32_t x = lw[h][0];
+#pragma unroll
+                        for (uint32_t w = 1; w < 4; w++) x = nw == w ? lw[h][w] : x;
+                        v = crc.partial(v, x, nb);
+                    }
+                    a.o.crc[tile * 64 + (uint32_t)jr[h]] = crc_mask(~v);
+                }
             }
         }
     }
 }
 
-template <int R>
-__global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<R>::kWords];
-    Crc4Lds<R>::fill(T);
-    __syncthreads();
-    const Crc4Lds<R> crc(T);
+// lane per record: the outputs that need no record bytes (the CRC and FNV-1 come from k_enc_pack):
+// final status, position, table-relative BlockHandle, table index, failed-add count
+__global__ __launch_bounds__(256) void k_enc_meta(EncArgs a) {
     const uint32_t ntab = (uint32_t)a.o.summary[1];
-    const uint64_t out_end = (uint64_t)a.out + a.out_cap;
     uint32_t failed = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-        const uint64_t kp = (uint64_t)a.keys + a.key_off[i];
-        const uint32_t klen = key_len_of(a, i);
-        // writer.go:246 (Add: FNV-1 of every key, before add()) / :249 (AddIkey: the caller's khash)
-        a.o.fnv1[i] = a.khash != nullptr ? a.khash[i] : fnv1_range(kp, klen, kp + klen);
         const uint32_t t = ntab ? table_of(a.o.table_start, ntab, i) : 0;
         a.o.table[i] = t;
         const uint64_t P = a.lens[i];
@@ -347,6 +435,13 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
             a.o.bh_len[i] = 0;
             a.o.crc[i] = 0;
             if (a.o.rec) a.o.rec[i] = bhg_handle{~0ull, 0, 0};
+            if (ntab == 0 && a.khash == nullptr) {  // k_enc_pack did not run: FNV-1 here
+                const uint64_t kp = (uint64_t)a.keys + a.key_off[i];
+                const uint32_t klen = key_len_of(a, i);
+                a.o.fnv1[i] = fnv1_range(kp, klen, kp + klen);
+            } else if (ntab == 0) {
+                a.o.fnv1[i] = a.khash[i];
+            }
             continue;
         }
         a.o.pos[i] = P;
@@ -354,7 +449,6 @@ __global__ __launch_bounds__(512) void k_enc_crc(EncArgs a) {
         a.o.bh_off[i] = (uint32_t)((t == 0 ? (uint64_t)a.init_size : 0ull) + (P - P0));
         a.o.bh_len[i] = L;
         if (a.o.rec) a.o.rec[i] = bhg_handle{P, L, 0};
-        a.o.crc[i] = crc_mask(~crc_range_a<8>(crc, 0xffffffffu, (uint64_t)a.out + P, L, out_end));
     }
     // summary[2]: failed adds (every status but OK / SKIPPED); one vector atomic per wave
     for (int d = 32; d >= 1; d >>= 1) failed += __shfl_xor(failed, d);
@@ -450,21 +544,19 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     a.key_len = E.key_len; a.pre_status = E.pre_status;
     a.single_table = E.single_table; a.max_tables = E.max_tables; a.init_size = E.init_size;
     a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
+    a.xtab = L.xtab;
     const uint32_t g = lane_grid(L, E.n, 256);
     hipLaunchKernelGGL(k_enc_sizes, dim3(g), dim3(256), 0, L.stream, a);
     hipError_t e = launch_exclusive_scan_u64(L, E.lens, E.lens, E.n, E.scan_scratch);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_enc_split, dim3(1), dim3(1024), 0, L.stream, a);
     uint32_t gp = (E.n + 64 * ENC_WAVES - 1) / (64 * ENC_WAVES);  // a wave per 64-record tile
-    const uint32_t capp = (uint32_t)L.num_cus * 8;
+    static const uint32_t per_cu = resident_per_cu((const void *)k_enc_pack, 64 * ENC_WAVES, 2);
+    const uint32_t capp = (uint32_t)L.num_cus * per_cu;
     if (gp > capp) gp = capp;
     if (gp == 0) gp = 1;
     hipLaunchKernelGGL(k_enc_pack, dim3(gp), dim3(64 * ENC_WAVES), 0, L.stream, a);
-    uint32_t gc = (E.n + 511) / 512;
-    const uint32_t capc = (uint32_t)L.num_cus * 2;
-    if (gc > capc) gc = capc;
-    if (gc == 0) gc = 1;
-    hipLaunchKernelGGL(k_enc_crc<16>, dim3(gc), dim3(512), 0, L.stream, a);
+    hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, a);
     if (E.o.table_size)
         hipLaunchKernelGGL(k_enc_tsize, dim3(lane_grid(L, E.max_tables, 256)), dim3(256), 0, L.stream, a);
     return hipGetLastError();

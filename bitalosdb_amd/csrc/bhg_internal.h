@@ -13,6 +13,7 @@ struct Launch {
     int num_cus;           // 256 on MI355X
     const uint32_t *ztab;  // device copy of build_tile_ztab() (owned by the context)
     const uint32_t *stab;  // device copy of build_stream_tab(128, 4) (owned by the context)
+    const uint32_t *xtab;  // device copy of build_xtab() (owned by the context)
 };
 
 // persistent grid for lane-per-item kernels: enough workgroups to fill the
