@@ -24,10 +24,13 @@ BHG_OK, BHG_EINVAL, BHG_EHIP, BHG_ENOMEM, BHG_ENODEV, BHG_ECAPACITY = 0, -1, -2,
 CODEC_NONE, CODEC_SNAPPY = 0, 1
 ST_OK, ST_RECORD_NIL, ST_ILLEGAL_LENGTH, ST_INCOMPLETE, ST_SNAPPY_CORRUPT, ST_SNAPPY_TOO_LARGE, \
     ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED, ST_NOT_FOUND, \
-    ST_NO_SPACE, ST_SKIPPED = range(13)
+    ST_NO_SPACE, ST_SKIPPED, ST_FILE_NUM_ZERO = range(14)
 ABI_VERSION = 2
 TABLE_DT = np.dtype([("base", "<u8"), ("index_off", "<u8"), ("index_len", "<u8"), ("conflict_off", "<u8"),
                      ("conflict_bh_off", "<u4"), ("conflict_bh_len", "<u4")])
+WRITER_INDEX_DT = np.dtype([("rec", "<u8"), ("sorted", "<u8"), ("sorted_kh", "<u8"), ("n", "<u4"),
+                            ("file_num", "<u4")])
+assert TABLE_DT.itemsize == 40 and WRITER_INDEX_DT.itemsize == 32
 
 EXPORTS = [
     "bhg_abi_version", "bhg_device_count", "bhg_create", "bhg_destroy", "bhg_last_error", "bhg_stream",
@@ -36,7 +39,8 @@ EXPORTS = [
     "bhg_crc32c_masked_batch", "bhg_crc32c_masked_long", "bhg_fnv32_batch", "bhg_encode_batch",
     "bhg_encode_ikey_batch", "bhg_scan_tables", "bhg_table_tail", "bhg_rebuild_tables",
     "bhg_repack_batch",
-    "bhg_host_register", "bhg_host_unregister", "bhg_get_batch",
+    "bhg_host_register", "bhg_host_unregister", "bhg_get_batch", "bhg_writer_index_build",
+    "bhg_bithash_get_batch",
 ]
 
 
@@ -100,6 +104,8 @@ def lib():
             "bhg_host_register": (I, [P, P, U64]),
             "bhg_host_unregister": (I, [P, P]),
             "bhg_get_batch": (I, [P, P, U64, P, U32, P, P, P, P, U32, P, P, P]),
+            "bhg_writer_index_build": (I, [P, P, U32, P, P, P]),
+            "bhg_bithash_get_batch": (I, [P, P, U64, P, U32, P, U32, P, P, U32, P, P, P, P, U32, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -38,6 +38,7 @@ STATUS_ERRORS = {
     B.ST_DATA_MAX_EXCEEDED: "bithash: panic add exceed data max size",
     B.ST_NOT_FOUND: "bithash: not found",                        # ErrBhNotFound
     B.ST_NO_SPACE: "bithash: encode output buffer too small",
+    B.ST_FILE_NUM_ZERO: "bithash: fileNum zero",                 # ErrBhFileNumZero
 }
 
 
@@ -232,6 +233,52 @@ class BithashCodec:
         rc = self.L.bhg_get_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(tab_t), ntables, _ptr(kb_t),
                                   _ptr(ko_t), _ptr(ti_t), _ptr(kh_t), n, _ptr(out_h), _ptr(out_s), self._stream())
         B.check(self.ctx, rc, "bhg_get_batch")
+
+    def writer_index(self, khash_t, n):
+        """bhg_writer_index_build: an open table's Writer.indexHash / conflictKeys as its records
+        sorted by khash (device int32 tensors sorted, sorted_kh)."""
+        with torch.cuda.stream(self.stream):
+            srt = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+            skh = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        rc = self.L.bhg_writer_index_build(self.ctx, _ptr(khash_t), n, _ptr(srt), _ptr(skh), self._stream())
+        B.check(self.ctx, rc, "bhg_writer_index_build")
+        return srt, skh
+
+    def bithash_get(self, src_t, writers, tables, fn_map, fn_table, keys, file_nums, khash=None):
+        """Bithash.Get over a batch (bhg_bithash_get_batch): the open writer of each query's
+        fileNum first (Writer.Get), then GetFileNumMap and Reader.Get on the mapped table.
+
+        writers: WRITER_INDEX_DT array (device pointers: record handles, writer_index outputs);
+        tables: TABLE_DT; fn_map / fn_table: per fileNum (dst fileNum or 0 / table index or
+        0xffffffff); keys: list of user keys.  Returns device tensors (handles as int64 pairs in
+        HANDLE_DT layout, status int32)."""
+        ko = np.zeros(len(keys) + 1, dtype=np.uint64)
+        ko[1:] = np.cumsum([len(k) for k in keys])
+        kb = b"".join(bytes(k) for k in keys)
+        n = len(keys)
+        dev = self.device
+
+        def t32(a):
+            a = np.ascontiguousarray(a, dtype=np.uint32)
+            return torch.from_numpy(a.view(np.int32).copy() if a.size else np.zeros(1, np.int32)).to(dev)
+
+        def tbytes(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            return torch.from_numpy(a.view(np.uint8).copy() if a.size else np.zeros(8, np.uint8)).to(dev)
+        with torch.cuda.stream(self.stream):
+            w_t = tbytes(writers, B.WRITER_INDEX_DT)
+            tab_t = tbytes(tables, B.TABLE_DT)
+            fm_t, ft_t, fn_t = t32(fn_map), t32(fn_table), t32(file_nums)
+            kb_t = torch.from_numpy(np.frombuffer(kb, np.uint8).copy() if len(kb) else np.zeros(1, np.uint8)).to(dev)
+            ko_t = torch.from_numpy(ko.view(np.int64)).to(dev)
+            kh_t = None if khash is None else t32(khash)
+            out_h = torch.empty(max(n, 1) * 2, dtype=torch.int64, device=dev)
+            out_s = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        rc = self.L.bhg_bithash_get_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(w_t), len(writers), _ptr(tab_t),
+                                          len(tables), _ptr(fm_t), _ptr(ft_t), len(fn_map), _ptr(kb_t), _ptr(ko_t),
+                                          _ptr(fn_t), _ptr(kh_t), n, _ptr(out_h), _ptr(out_s), self._stream())
+        B.check(self.ctx, rc, "bhg_bithash_get_batch")
+        return out_h[:2 * n], out_s[:n]
 
     def crc_masked_bytes(self, b):
         """crc.New(b).Value() of one host byte string, on the GPU (bhg_crc32c_masked_batch)."""

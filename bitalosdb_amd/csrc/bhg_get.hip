@@ -174,6 +174,30 @@ __device__ void seek_conflict(uint64_t blk, uint32_t blen, uint64_t key, uint32_
     }
 }
 
+// Reader.Get's index path on one opened table: status OK / NOT_FOUND / ILLEGAL_LENGTH and the
+// handle rebased to src
+__device__ __forceinline__ uint32_t table_lookup(uint64_t base, uint64_t src_len, const bhg_table &t, uint64_t kp,
+                                                 uint32_t klen, uint32_t kh, bhg_handle &h) {
+    uint64_t v;
+    const bool idx_ok = t.index_off <= src_len && t.index_len <= src_len - t.index_off;
+    if (!(idx_ok && get64(base + t.index_off, t.index_len, kh, v))) return BHG_ST_NOT_FOUND;
+    uint32_t bo = (uint32_t)v, bl = (uint32_t)(v >> 32);  // LE handle bytes (reader.go:215-217)
+    if (t.conflict_bh_len != 0 && bo >= t.conflict_bh_off && bl <= t.conflict_bh_len) {
+        const bool cf_ok = t.conflict_off <= src_len && t.conflict_bh_len <= src_len - t.conflict_off;
+        if (cf_ok) seek_conflict(base + t.conflict_off, t.conflict_bh_len, kp, klen, bo, bl);
+        else bo = bl = 0;
+        if (bo == 0 && bl == 0) return BHG_ST_ILLEGAL_LENGTH;  // reader.go:224-226
+    }
+    h = bhg_handle{t.base + bo, bl, 0};
+    return BHG_ST_OK;
+}
+
+__device__ __forceinline__ uint32_t query_hash(uint64_t kp, uint32_t klen) {
+    uint32_t kh = BHG_FNV_OFFSET;
+    for (uint32_t b = 0; b < klen; b++) kh = (kh * BHG_FNV_PRIME) ^ ld8(kp + b);
+    return kh;
+}
+
 template <bool HAVE_HASH>
 __global__ __launch_bounds__(256) void k_get(const uint8_t *__restrict__ src, uint64_t src_len,
                                              const bhg_table *__restrict__ tables, uint32_t ntables,
@@ -188,32 +212,120 @@ __global__ __launch_bounds__(256) void k_get(const uint8_t *__restrict__ src, ui
         const uint32_t klen = (uint32_t)(k1 - k0);
         bhg_handle h = {0, 0, 0};
         uint32_t st = BHG_ST_NOT_FOUND;
-        if (ti < ntables) {
-            const bhg_table t = tables[ti];
-            uint32_t kh;
-            if (HAVE_HASH) {
-                kh = khash[i];
-            } else {
-                kh = BHG_FNV_OFFSET;
-                for (uint32_t b = 0; b < klen; b++) kh = (kh * BHG_FNV_PRIME) ^ ld8(kp + b);
+        if (ti < ntables) st = table_lookup(base, src_len, tables[ti], kp, klen, HAVE_HASH ? khash[i] : query_hash(kp, klen), h);
+        out_h[i] = h;
+        out_st[i] = st;
+    }
+}
+
+// the user key of a stored record (ikeySize at +0, UserKey at +12; ikeySize < 8 -> empty)
+__device__ __forceinline__ void rec_user_key(uint64_t p, uint64_t end, uint64_t &kp, uint32_t &kl) {
+    const uint32_t ik = p + 4 <= end ? ldu32(p, end) : 0u;
+    kl = ik >= 8 ? ik - 8 : 0u;
+    kp = p + 12;
+    if (kp + kl > end) kl = 0;
+}
+
+__device__ __forceinline__ bool keq(uint64_t a, uint32_t al, uint64_t b, uint32_t bl) {
+    return al == bl && bcmp(a, al, b, bl) == 0;
+}
+
+// Writer.Get's index (writer.go:171-228 over the state updateHash leaves, :285-310): the khash run
+// of the sorted record list; one distinct UserKey in the run -> ih.bh = the last add, whatever
+// the queried key; two or more (conflict) -> conflictKeys[key] = the last add of that key, or
+// nothing.  Returns true with the handle when Writer.Get would read a record.
+__device__ bool writer_lookup(uint64_t base, uint64_t end, const bhg_writer_index &w, uint64_t kp, uint32_t klen,
+                              uint32_t kh, bhg_handle &h) {
+    const bhg_handle *rec = reinterpret_cast<const bhg_handle *>(w.rec);
+    const uint32_t *sorted = reinterpret_cast<const uint32_t *>(w.sorted);
+    const uint32_t *skh = reinterpret_cast<const uint32_t *>(w.sorted_kh);
+    uint32_t lo = 0, hi = w.n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (skh[m] < kh) lo = m + 1; else hi = m;
+    }
+    uint32_t e = lo;
+    while (e < w.n && skh[e] == kh) e++;
+    if (e == lo) return false;  // indexHash has no entry: bh zero
+    const bhg_handle last = rec[sorted[e - 1]];
+    uint64_t lk; uint32_t ll;
+    rec_user_key(base + last.offset, end, lk, ll);
+    bool conflict = false;
+    for (uint32_t q = lo; q + 1 < e && !conflict; q++) {
+        uint64_t qk; uint32_t ql;
+        rec_user_key(base + rec[sorted[q]].offset, end, qk, ql);
+        conflict = !keq(lk, ll, qk, ql);
+    }
+    bhg_handle bh = {0, 0, 0};
+    if (!conflict) {
+        bh = last;
+    } else {
+        for (uint32_t q = e; q > lo; q--) {
+            const bhg_handle r = rec[sorted[q - 1]];
+            uint64_t qk; uint32_t ql;
+            rec_user_key(base + r.offset, end, qk, ql);
+            if (keq(kp, klen, qk, ql)) { bh = r; break; }
+        }
+    }
+    if (bh.length == 0) return false;  // bh.Length <= 0: (nil, nil, nil)
+    h = bh;
+    return true;
+}
+
+// Bithash.Get (bithash.go:101-119): the open writer of file_num first (Writer.Get), then
+// GetFileNumMap(fn) (:264-273; 0 -> ErrBhFileNumZero) and Reader.Get on that table
+template <bool HAVE_HASH>
+__global__ __launch_bounds__(256) void k_bithash_get(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                     const bhg_writer_index *__restrict__ writers, uint32_t nwriters,
+                                                     const bhg_table *__restrict__ tables, uint32_t ntables,
+                                                     const uint32_t *__restrict__ fn_map,
+                                                     const uint32_t *__restrict__ fn_table, uint32_t fn_count,
+                                                     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
+                                                     const uint32_t *__restrict__ file_nums,
+                                                     const uint32_t *__restrict__ khash, uint32_t n,
+                                                     bhg_handle *__restrict__ out_h, uint32_t *__restrict__ out_st) {
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t fn = file_nums[i];
+        const uint64_t k0 = key_off[i], k1 = key_off[i + 1];
+        const uint64_t kp = (uint64_t)keys + k0;
+        const uint32_t klen = (uint32_t)(k1 - k0);
+        const uint32_t kh = HAVE_HASH ? khash[i] : query_hash(kp, klen);
+        bhg_handle h = {0, 0, 0};
+        uint32_t st = BHG_ST_NOT_FOUND;
+        bool done = false;
+        for (uint32_t w = 0; w < nwriters && !done; w++) {
+            const bhg_writer_index W = writers[w];
+            if (W.file_num == fn) {
+                done = writer_lookup(base, end, W, kp, klen, kh, h);
+                if (done) st = BHG_ST_OK;
+                break;
             }
-            uint64_t v;
-            const bool idx_ok = t.index_off <= src_len && t.index_len <= src_len - t.index_off;
-            if (idx_ok && get64(base + t.index_off, t.index_len, kh, v)) {
-                uint32_t bo = (uint32_t)v, bl = (uint32_t)(v >> 32);  // LE handle bytes (reader.go:215-217)
-                st = BHG_ST_OK;
-                if (t.conflict_bh_len != 0 && bo >= t.conflict_bh_off && bl <= t.conflict_bh_len) {
-                    const bool cf_ok = t.conflict_off <= src_len && t.conflict_bh_len <= src_len - t.conflict_off;
-                    if (cf_ok) seek_conflict(base + t.conflict_off, t.conflict_bh_len, kp, klen, bo, bl);
-                    else bo = bl = 0;
-                    if (bo == 0 && bl == 0) st = BHG_ST_ILLEGAL_LENGTH;  // reader.go:224-226
-                }
-                if (st == BHG_ST_OK) h = bhg_handle{t.base + bo, bl, 0};
+        }
+        if (!done) {
+            const uint32_t dst = fn < fn_count ? fn_map[fn] : 0u;
+            if (dst == 0) {
+                st = BHG_ST_FILE_NUM_ZERO;
+            } else {
+                const uint32_t ti = dst < fn_count ? fn_table[dst] : 0xffffffffu;
+                if (ti < ntables) st = table_lookup(base, src_len, tables[ti], kp, klen, kh, h);
             }
         }
         out_h[i] = h;
         out_st[i] = st;
     }
+}
+
+// record i's khash -> sort key (stable radix sort by the low 32 bits)
+__global__ __launch_bounds__(256) void k_widx_keys(const uint32_t *__restrict__ khash, uint32_t n, uint64_t *keys,
+                                                   uint32_t *idx) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        keys[i] = khash[i];
+        idx[i] = i;
+    }
+}
+__global__ __launch_bounds__(256) void k_widx_lo(const uint64_t *__restrict__ keys, uint32_t n, uint32_t *out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = (uint32_t)keys[i];
 }
 
 }  // namespace
@@ -231,6 +343,48 @@ hipError_t launch_get(const Launch &L, const uint8_t *src, uint64_t src_len, con
     else
         hipLaunchKernelGGL(k_get<false>, dim3(grid), dim3(256), 0, L.stream, src, src_len, tables, ntables, keys,
                            key_off, table_idx, khash, n, out_h, out_st);
+    return hipGetLastError();
+}
+
+hipError_t launch_bithash_get(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
+                              uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
+                              const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
+                              const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_h,
+                              uint32_t *out_st) {
+    uint64_t need = (n + 255) / 256;
+    uint64_t cap = (uint64_t)L.num_cus * 16;
+    uint32_t grid = (uint32_t)(need < cap ? need : cap);
+    if (grid == 0) grid = 1;
+    if (khash)
+        hipLaunchKernelGGL(k_bithash_get<true>, dim3(grid), dim3(256), 0, L.stream, src, src_len, writers, nwriters,
+                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, n, out_h, out_st);
+    else
+        hipLaunchKernelGGL(k_bithash_get<false>, dim3(grid), dim3(256), 0, L.stream, src, src_len, writers, nwriters,
+                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, n, out_h, out_st);
+    return hipGetLastError();
+}
+
+size_t writer_index_scratch_bytes(uint32_t n) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return al(radix_sort_scratch_bytes(n)) + 2 * al((size_t)n * 8) + al((size_t)n * 4);
+}
+
+hipError_t launch_writer_index(const Launch &L, const uint32_t *khash, uint32_t n, uint32_t *sorted,
+                               uint32_t *sorted_kh, void *scratch) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    uint8_t *s = reinterpret_cast<uint8_t *>(scratch);
+    void *sort_buf = s;
+    s += al(radix_sort_scratch_bytes(n));
+    uint64_t *k = reinterpret_cast<uint64_t *>(s);
+    s += al((size_t)n * 8);
+    uint64_t *ks = reinterpret_cast<uint64_t *>(s);
+    s += al((size_t)n * 8);
+    uint32_t *idx = reinterpret_cast<uint32_t *>(s);
+    const uint32_t g = lane_grid(L, n ? n : 1, 256);
+    hipLaunchKernelGGL(k_widx_keys, dim3(g), dim3(256), 0, L.stream, khash, n, k, idx);
+    hipError_t e = launch_radix_sort_pairs(L, k, ks, idx, sorted, n, 32, sort_buf);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_widx_lo, dim3(g), dim3(256), 0, L.stream, ks, n, sorted_kh);
     return hipGetLastError();
 }
 

@@ -71,6 +71,8 @@ extern "C" {
                                       nothing was written for it -- grow the buffer and re-run */
 #define BHG_ST_SKIPPED 12          /* encode: live[i] == 0, the compaction filter dropped the record
                                       (bitree/bithash.go:225-228); not an error */
+#define BHG_ST_FILE_NUM_ZERO 13    /* Bithash.Get: GetFileNumMap(fn) == 0 -> ErrBhFileNumZero
+                                      (bithash.go:109-111, 264-273) */
 
 /* BlockHandle (block.go:26-39) with the offset widened to 64 bits so one
  * batch may span many concatenated/mmap'd table files. 16 B. */
@@ -362,6 +364,43 @@ typedef struct bhg_table {
 int bhg_get_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_table *tables, uint32_t ntables,
                   const uint8_t *keys, const uint64_t *key_off, const uint32_t *table_idx, const uint32_t *khash,
                   uint32_t n, bhg_handle *out_handles, uint32_t *out_status, void *stream);
+
+/* ---- Bithash.Get over open (mutable) tables, the fileNum map and opened tables (device) ----
+ * An open table's index: Writer.indexHash + conflictKeys (writer.go:285-310) of a table still
+ * being written, held as its records sorted by khash (stable: add order inside a khash).
+ * Built by bhg_writer_index_build from the records' khash (bhg_encode_batch's fnv1 output, or
+ * the AddIkey khash).  Writer.Get (writer.go:171-228) on it: a khash whose adds all carried one
+ * UserKey answers the last add (ih.bh, whatever key is queried, as Go does); two or more
+ * distinct keys (conflict) answer the last add of the queried key (conflictKeys) or nothing.
+ *   rec       : device bhg_handle[n], the records in add order (offsets into src)
+ *   sorted    : device uint32_t[n] record indices sorted by khash
+ *   sorted_kh : device uint32_t[n] khash of sorted[j]
+ *   file_num  : the writer's fileNum (the rwwWriters key, bithash.go:102)         32 B */
+typedef struct bhg_writer_index {
+    uint64_t rec;
+    uint64_t sorted;
+    uint64_t sorted_kh;
+    uint32_t n;
+    uint32_t file_num;
+} bhg_writer_index;
+
+/* sorted / sorted_kh of an open table from its records' khash[n] (device pointers). */
+int bhg_writer_index_build(bhg_ctx *ctx, const uint32_t *khash, uint32_t n, uint32_t *sorted, uint32_t *sorted_kh,
+                           void *stream);
+
+/* Bithash.Get (bithash.go:101-119) for n queries (UserKey keys[key_off[i] : key_off[i+1]],
+ * khash[i] or hash.Fnv32 of the key when khash is null, fileNum file_nums[i]):
+ *   1. the open writer with that fileNum (writers[], nwriters): Writer.Get -> OK on a hit;
+ *   2. dst = fn_map[fn] (GetFileNumMap, :264-273; fn >= fn_count or 0 -> BHG_ST_FILE_NUM_ZERO);
+ *   3. the opened table tables[fn_table[dst]] (bhtReaders; none -> BHG_ST_NOT_FOUND): Reader.Get's
+ *      index path as bhg_get_batch (OK / NOT_FOUND / ILLEGAL_LENGTH).
+ * out_handles[i] is rebased to src (feed to bhg_decode_batch for readData / Writer.Get's read).
+ * fn_map and fn_table are indexed by fileNum, fn_count entries each.  All pointers device. */
+int bhg_bithash_get_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
+                          uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
+                          const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
+                          const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_handles,
+                          uint32_t *out_status, void *stream);
 
 #ifdef __cplusplus
 }

@@ -409,6 +409,49 @@ def _writer_get(w, ukey):
     return _read_data(bytes(w.file), bh, w.compressor)
 
 
+def writer_get_handle(w, ukey, khash=None):
+    """Writer.Get's index (writer.go:171-228): the handle it reads, or None (bh.Length <= 0)."""
+    ih = w.index_hash.get(O.fnv32(ukey) if khash is None else khash)
+    if ih is None:
+        return None
+    bh = w.conflict_keys.get(bytes(ukey), (0, 0)) if ih[2] else ih[0]
+    return bh if bh[1] > 0 else None
+
+
+def bithash_get_handle(writers, files, fn_map, ukey, fn, khash=None):
+    """Bithash.Get (bithash.go:101-119) without the read: writers = {fileNum: open Writer}
+    (rwwWriters), files = {fileNum: closed table bytes} (bhtReaders), fn_map = GetFileNumMap's map.
+    Returns (status, fileNum, (off, len)) with status "OK", "NOT_FOUND", "ILLEGAL_LENGTH" or
+    "FILE_NUM_ZERO"; a writer hit is final (its records are well formed)."""
+    w = writers.get(fn)
+    if w is not None:
+        bh = writer_get_handle(w, ukey, khash)
+        if bh is not None:
+            return "OK", fn, bh
+    dst = fn_map.get(fn, 0)
+    if dst == 0:
+        return "FILE_NUM_ZERO", 0, (0, 0)
+    if dst not in files:
+        return "NOT_FOUND", dst, (0, 0)
+    st, off, ln = get_handle(files[dst], ukey) if khash is None else _get_handle_kh(files[dst], ukey, khash)
+    return st, dst, (off, ln)
+
+
+def _get_handle_kh(f, ukey, khash):
+    t = open_table(f)
+    v = hash_index_get64(t["index_data"], khash)
+    if v is None:
+        return "NOT_FOUND", 0, 0
+    off, length = v & 0xFFFFFFFF, v >> 32
+    coff, clen = t["conflict_bh"]
+    if clen != 0 and off >= coff and length <= clen:
+        uk, cv = block_seek_ge(t["conflict_buf"], bytes(ukey))
+        off, length = decode_bh(cv) if cv is not None and uk == bytes(ukey) else (0, 0)
+        if (off, length) == (0, 0):
+            return "ILLEGAL_LENGTH", 0, 0
+    return "OK", off, length
+
+
 def read_footer(f):
     """readTableFooter + decodeTableFooter (table.go:90-127)."""
     if len(f) < FOOTER_LEN:

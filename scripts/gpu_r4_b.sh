@@ -8,7 +8,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 120 scripts/lab/c2_r4/dma_lab 30 > $O/dma_lab.txt 2>&1; echo "dma_lab rc=$?" >> $O/dma_lab.txt
 cat $O/dma_lab.txt
-timeout -k 10 600 python -u -m pytest tests/test_gpu_encode.py tests/test_gpu_compaction.py tests/test_gpu_tail.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread > $O/pytest_enc.txt 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_get.py tests/test_gpu_encode.py tests/test_gpu_compaction.py tests/test_gpu_tail.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread > $O/pytest_enc.txt 2>&1; rc=$?
 tail -3 $O/pytest_enc.txt
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py --config c4 --no-cpu > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench c4 failed"; tail -5 $O/bench_c4.err; exit 1; }

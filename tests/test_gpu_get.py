@@ -162,3 +162,87 @@ def test_given_khash_matches(codec):
     codec.sync()
     assert torch.equal(h1, h2) and torch.equal(s1, s2)
     assert (s1.cpu().numpy() == ST_OK).all()
+
+
+def test_bithash_get_open_writer_and_filenum_map(codec):
+    """Bithash.Get (bithash.go:101-119) over a batch (bhg_bithash_get_batch): queries on a
+    still-open table go through Writer.Get's in-memory index (writer.go:171-228, rebuilt on
+    the device by bhg_writer_index_build) -- overwritten keys answer the last add, the K2
+    collision pairs added to the open table take the conflictKeys path, a never-written key
+    sharing a non-conflict khash answers the stored key's handle as Go does; writer misses fall
+    through GetFileNumMap to the closed tables (a compacted fileNum remapped to its
+    destination, an unmapped fileNum -> ErrBhFileNumZero).  Checked against the restated
+    Bithash.Get (oracle/table.py bithash_get_handle)."""
+    from bitalosdb_amd._lib import ST_FILE_NUM_ZERO, WRITER_INDEX_DT
+    from bitalosdb_amd.codec import handles_tensor
+    rng = random.Random(77)
+    keys2 = _k2_keys()
+    k2 = open(os.path.join(GOLD, "k2.bht"), "rb").read()
+    f5, w5 = _writer_table(rng, 300, 5)
+    f6, w6 = _writer_table(rng, 300, 6)
+    files = {3: k2, 5: f5, 6: f6}
+    order = [3, 5, 6]
+    src, tabs = _concat([files[fn] for fn in order])
+    # the open table (fileNum 8): plain keys with overwrites, two K2 collision pairs (conflict), and
+    # one key of a third pair alone (a non-conflict khash shared with a never-written key)
+    w = T.Writer(8, 1 << 30)
+    plain = [bytes(rng.randrange(97, 123) for _ in range(rng.choice([5, 16, 32]))) for _ in range(150)]
+    adds = plain + plain[:40] + keys2[:4] + [keys2[0], keys2[3]] + [keys2[4]]
+    rng.shuffle(adds)
+    for i, k in enumerate(adds):
+        w.add(k, ((i + 1) << 8) | 1, bytes(rng.randrange(65, 91) for _ in range(rng.choice([3, 60, 400]))))
+    wbase = len(src) + 3
+    src = src + bytes(3) + bytes(w.file)
+    recs = []
+    off = 0
+    for k in adds:                                   # the writer's records in add order
+        ln = 12 + len(k) + 8 + struct_len(w.file, off)
+        recs.append((wbase + off, ln, 0))
+        off += ln
+    rec_h = np.array(recs, dtype=O.HANDLE_DT)
+    dev = codec.device
+    with torch.cuda.stream(codec.stream):
+        src_t = torch.from_numpy(np.frombuffer(src, np.uint8).copy()).to(dev)
+        rec_t = handles_tensor(rec_h, dev)
+        kh_t = torch.from_numpy(np.array([O.fnv32(k) for k in adds], dtype=np.uint32).view(np.int32)).to(dev)
+        srt, skh = codec.writer_index(kh_t, len(adds))
+    writers = np.zeros(1, dtype=WRITER_INDEX_DT)
+    writers[0] = (rec_t.data_ptr(), srt.data_ptr(), skh.data_ptr(), len(adds), 8)
+    fn_map_d = {3: 3, 4: 6, 5: 5, 6: 6, 8: 8}          # 4 was compacted into 6; 7 is unmapped
+    fn_count = 10
+    fn_map = np.zeros(fn_count, np.uint32)
+    for s_, d_ in fn_map_d.items():
+        fn_map[s_] = d_
+    fn_table = np.full(fn_count, 0xFFFFFFFF, np.uint32)
+    for ti, fn in enumerate(order):
+        fn_table[fn] = ti
+    missing = [bytes(rng.randrange(97, 123) for _ in range(12)) for _ in range(60)]
+    qs = [(8, k) for k in plain + keys2 + missing]
+    qs += [(5, k) for k in w5[:100]] + [(4, k) for k in w6[:100]] + [(6, k) for k in missing[:20]]
+    qs += [(3, k) for k in keys2] + [(7, k) for k in plain[:10]] + [(12, k) for k in plain[:5]]
+    rng.shuffle(qs)
+    h_t, s_t = codec.bithash_get(src_t, writers, tabs, fn_map, fn_table, [q[1] for q in qs], [q[0] for q in qs])
+    codec.sync()
+    h = h_t.cpu().numpy().view(np.uint8).view(O.HANDLE_DT)
+    st = s_t.cpu().numpy().view(np.uint32)
+    code = dict(ST, FILE_NUM_ZERO=ST_FILE_NUM_ZERO)
+    base_of = {fn: int(tabs["base"][ti]) for ti, fn in enumerate(order)}
+    base_of[8] = wbase
+    seen = set()
+    for i, (fn, k) in enumerate(qs):
+        es, efn, (eo, el) = T.bithash_get_handle({8: w}, files, fn_map_d, k, fn)
+        assert st[i] == code[es], (i, fn, k, es, st[i])
+        if es == "OK":
+            assert int(h["offset"][i]) == base_of[efn] + eo and int(h["length"][i]) == el, (i, fn, k)
+            seen.add((fn == 8, efn == 8))
+    assert (True, True) in seen and (False, False) in seen          # writer hits and table hits
+    assert {code["FILE_NUM_ZERO"], code["NOT_FOUND"]} <= set(st.tolist())
+    # the conflict path ran: the two K2 pairs added to the open table answer their own records
+    for k in keys2[:4]:
+        es, efn, bh = T.bithash_get_handle({8: w}, files, fn_map_d, k, 8)
+        assert es == "OK" and efn == 8 and w.index_hash[O.fnv32(k)][2]
+
+
+def struct_len(buf, off):
+    import struct
+    return struct.unpack_from("<I", buf, off + 4)[0]
