@@ -16,3 +16,5 @@ python -c "
 import json; d=json.load(open('$O/bench_c4.json')); r=d['roofline']
 print('c4', d['value'], d['ms_per_step'], r['frac'], r.get('traffic_ratio'), [(k, v['value']) for k, v in d.items() if k.startswith('secondary')])
 print(json.dumps({k: v for k, v in r.get('traffic_by_kernel', {}).items()}))"
+timeout -k 10 300 python -u bench.py --config tail --steps 5 --warmup 2 > $O/bench_tail.json 2> $O/bench_tail.err || { echo "bench tail failed"; tail -5 $O/bench_tail.err; exit 1; }
+cat $O/bench_tail.json

@@ -30,6 +30,8 @@
 #include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
 #include "../../../bitalosdb_amd/csrc/bhg_device.h"
 #include "../../../include/bithashgpu.h"
+#include "../../../bitalosdb_amd/csrc/bhg_decode_dma.hip"  // the product kernels, timed beside the lab one
+#include "../../../bitalosdb_amd/csrc/bhg_decode_tile.hip"
 
 #define CK(x)                                                                                  \
     do {                                                                                       \
@@ -136,7 +138,7 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) { return readfirstlane_u64(x); }
 
-template <int NW, int D>
+template <int NW, int D, int WORK = 1>
 __global__ __launch_bounds__(64 * NW) void k_decode_dma(const uint8_t *__restrict__ src, uint64_t src_len,
                                                        const bhg_handle *__restrict__ handles, uint32_t n,
                                                        const uint32_t *__restrict__ expected_crc,
@@ -206,8 +208,7 @@ __global__ __launch_bounds__(64 * NW) void k_decode_dma(const uint8_t *__restric
     };
     // issue group g's DMA into slot g % D; returns the VM-op count after it
     uint32_t ops = 0;
-    auto issue = [&](uint32_t g) {
-        const GInfo q = ginfo(g, false);
+    auto issue = [&](uint32_t g, const GInfo &q) {
         const uint32_t slot = ring + (g % D) * SLOT;
         uint32_t off[G], pc[G + 1];
         layout(q, off, pc);
@@ -233,11 +234,13 @@ __global__ __launch_bounds__(64 * NW) void k_decode_dma(const uint8_t *__restric
 
     static_assert(D == 3, "ring rotation below is written for 3 slots");
     uint32_t o0 = 0, o1 = 0, o2 = 0;   // VM-op counts after groups g, g+1, g+2 were issued
-    if (ngroups > 0) o0 = issue(0);
-    if (ngroups > 1) o1 = issue(1);
+    if (ngroups > 0) o0 = issue(0, ginfo(0, false));
+    if (ngroups > 1) o1 = issue(1, ginfo(1, false));
+    GInfo qd = ginfo(2, false);         // the next DMA group's info, loaded one iteration ahead
     GInfo qc = ginfo(0, true);          // group g's info, loaded one iteration ahead
     for (uint32_t g = 0; g < ngroups; g++) {
-        if (g + 2 < ngroups) o2 = issue(g + 2);
+        if (g + 2 < ngroups) o2 = issue(g + 2, qd);
+        if (g + 3 < ngroups) qd = ginfo(g + 3, false);
         wait_vm(ops - o0);
         const GInfo q = qc;
         if (g + 1 < ngroups) qc = ginfo(g + 1, true);
@@ -256,6 +259,7 @@ __global__ __launch_bounds__(64 * NW) void k_decode_dma(const uint8_t *__restric
         uint32_t acc = 0;
         const uint32_t Lal = L;  // (aligned path: (R0 + L) % 4 == 0 for every record of the wave)
         bool firstw = true;
+        if (!WORK) e = -1;  // floor probe: the DMA ring, parse and stores without the window CRCs
         while (__ballot(e >= 0)) {
             if (e >= 0) {
                 const uint32_t A = R0 + Lal - WB * (uint32_t)(e + 1);
@@ -413,10 +417,28 @@ static inline uint64_t rnd() {
     return rng_state;
 }
 
-template <int NW, int D>
+template <int NW, int D, int WORK = 1>
 static void launch(const uint8_t *src, uint64_t len, const bhg_handle *h, uint32_t n, const uint32_t *ec, bhg_desc *out,
                    const uint32_t *gz, int cus, hipStream_t s) {
-    hipLaunchKernelGGL((dl::k_decode_dma<NW, D>), dim3(cus), dim3(64 * NW), 0, s, src, len, h, n, ec, out, gz);
+    hipLaunchKernelGGL((dl::k_decode_dma<NW, D, WORK>), dim3(cus), dim3(64 * NW), 0, s, src, len, h, n, ec, out, gz);
+}
+
+static uint32_t *g_xtab = nullptr;
+static void launch_product(const uint8_t *src, uint64_t len, const bhg_handle *h, uint32_t n, const uint32_t *ec,
+                           bhg_desc *out, const uint32_t *, int cus, hipStream_t s) {
+    bhg::Launch L;
+    L.stream = s; L.num_cus = cus; L.ztab = nullptr; L.stab = nullptr; L.xtab = g_xtab;
+    CK(bhg::launch_decode_dma(L, src, len, h, n, 0, ec, out, nullptr));
+}
+
+static uint32_t *g_ztab = nullptr;
+template <int BAL>
+static void launch_tile(const uint8_t *src, uint64_t len, const bhg_handle *h, uint32_t n, const uint32_t *ec,
+                        bhg_desc *out, const uint32_t *, int cus, hipStream_t s) {
+    const uint64_t tiles = (n + 63) / 64;
+    uint64_t need = (tiles + 7) / 8;
+    uint32_t grid = (uint32_t)(need < (uint64_t)cus ? need : cus);
+    hipLaunchKernelGGL((bhg::k_decode_tile<8, 2, BAL>), dim3(grid), dim3(512), 0, s, src, len, h, n, ec, out, g_ztab);
 }
 
 int main(int argc, char **argv) {
@@ -461,7 +483,23 @@ int main(int argc, char **argv) {
     if (n > 30) { uint32_t x; CK(hipMemcpy(&x, ec + 29, 4, hipMemcpyDeviceToHost)); x ^= 1; CK(hipMemcpy(ec + 29, &x, 4, hipMemcpyHostToDevice)); }
     typedef void (*lfn)(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *, const uint32_t *, int, hipStream_t);
     struct V { const char *name; lfn fn; };
-    const V vs[] = {{"dma_w8_d3", launch<8, 3>}};
+    static uint32_t *xt = nullptr;
+    if (!xt) {
+        std::vector<uint32_t> x(1024u * XTAB_N);
+        build_xtab(x.data());
+        CK(hipMalloc(&xt, x.size() * 4));
+        CK(hipMemcpy(xt, x.data(), x.size() * 4, hipMemcpyHostToDevice));
+    }
+    g_xtab = xt;
+    if (!g_ztab) {
+        std::vector<uint32_t> zt(kZTabWords);
+        build_tile_ztab(zt.data());
+        CK(hipMalloc(&g_ztab, zt.size() * 4));
+        CK(hipMemcpy(g_ztab, zt.data(), zt.size() * 4, hipMemcpyHostToDevice));
+    }
+    const V vs[] = {{"tile_bal0", launch_tile<0>}, {"tile_bal1", launch_tile<1>}, {"tile_bal0_again", launch_tile<0>},
+                    {"tile_bal1_again", launch_tile<1>},{"dma_w8_d3_pf", launch<8, 3>},
+                    {"floor_w8_nocrc", launch<8, 3, 0>}};
     auto prod = [&]() { if (bhg_decode_batch(ctx, src, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
     for (int it = 0; it < 200; it++) prod();  // clocks
     CK(hipStreamSynchronize(s));
