@@ -188,10 +188,10 @@ inline void build_tile_ztab(uint32_t *out) {
 }
 
 // Shift tables of the kernels built on CrcR8 (bhg_device.h): the pack kernel's chunk combine
-// (Z_16 .. Z_1024, powers of two) and the 68-B-window decode (Z_32, Z_68 .. Z_1088).  One device
-// array owned by the context, 1024 words per table in this order.
-enum XTab : uint32_t { XZ16, XZ32, XZ64, XZ128, XZ256, XZ512, XZ1024, XZ68, XZ136, XZ272, XZ544, XZ1088, XTAB_N };
-constexpr uint64_t kXTabLen[XTAB_N] = {16, 32, 64, 128, 256, 512, 1024, 68, 136, 272, 544, 1088};
+// (Z_16 .. Z_1024, powers of two).  One device array owned by the context, 1024 words per table
+// in this order.
+enum XTab : uint32_t { XZ16, XZ32, XZ64, XZ128, XZ256, XZ512, XZ1024, XTAB_N };
+constexpr uint64_t kXTabLen[XTAB_N] = {16, 32, 64, 128, 256, 512, 1024};
 inline void build_xtab(uint32_t *out) {
     for (uint32_t k = 0; k < XTAB_N; k++) crc32c_shift_table(kXTabLen[k], out + 1024 * k);
 }

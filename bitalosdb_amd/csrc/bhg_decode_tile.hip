@@ -45,8 +45,6 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-__device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-
 __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
     return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
 }
@@ -56,7 +54,7 @@ __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
 // NCH: interleaved CRC chains per 128-B window (1, 2 or 4), folded with Z_{128/NCH}.  With
 // 2 waves per SIMD and a round's loads in flight, one chain's 32 dependent steps hide behind
 // memory; every fold costs a conflicted shift-table lookup.
-template <int WPB, int NCH, int BAL = 0>
+template <int WPB, int NCH>
 __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restrict__ src, uint64_t src_len,
                                                           const bhg_handle *__restrict__ handles, uint32_t n,
                                                           const uint32_t *__restrict__ expected_crc,
@@ -79,32 +77,22 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     const Crc4Perm crc(T);
     const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
     const uint64_t base = (uint64_t)src, end = base + src_len;
-    // BAL 0: wave-major 64-record tiles over the whole batch.  BAL 1: wave w owns the contiguous
-    // records [r0, r0 + cnt), an equal share (+-1), cut into 64-record tiles: every wave finishes
-    // within one partial tile of the others (with whole tiles dealt round-robin, 7.63 tiles per
-    // wave at C2 meant 8 tile times for all)
-    const uint32_t lanew = uni32(threadIdx.x >> 6);
-    const uint32_t gw = lanew * gridDim.x + blockIdx.x, nwt = gridDim.x * WPB;
-    const uint32_t per = n / nwt, rem = n % nwt;
-    const uint32_t r0 = BAL ? gw * per + (gw < rem ? gw : rem) : 0u;
-    const uint32_t cnt = BAL ? per + (gw < rem ? 1u : 0u) : n;
-    const uint32_t ntiles = BAL ? (cnt + 63) / 64 : (n + 63) / 64;
-    const uint32_t tstride = BAL ? 1u : gridDim.x * WPB;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
     // wave-major tile index: the waves that take one tile more than the others
     // (ntiles mod tstride of them) are spread over every CU, not packed on the first ones
-    uint32_t tile = BAL ? 0u : (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     bhg_handle hn = {0, 0, 0};
-    if (tile < ntiles && tile * 64 + lane < cnt) hn = handles[r0 + tile * 64 + lane];
+    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
     for (; tile < ntiles; tile += tstride) {
         // ---------------- phase 1: lane = record (Reader.readData's checks, readRecord, readKV)
         const bhg_handle h = hn;
-        const uint32_t il = tile * 64 + lane;  // index inside this wave's range (BAL) or the batch
-        const uint32_t i = r0 + il;
+        const uint32_t i = tile * 64 + lane;
         {
             const uint32_t tn = tile + tstride;
-            if (tn < ntiles && tn * 64 + lane < cnt) hn = handles[r0 + tn * 64 + lane];
+            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
         }
-        const bool valid = il < cnt;
+        const bool valid = i < n;
         // requested here, used after phase 2: a load issued at the end would expose its latency per tile
         const uint32_t ecrc = (expected_crc != nullptr && valid) ? expected_crc[i] : 0u;
         uint32_t st = BHG_ST_OK;

@@ -52,9 +52,6 @@ hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, 
 // bhg_decode_tile.hip: the NoCompressor decode kernel
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out);
-// bhg_decode_dma.hip: the LDS-DMA stream decode; mode 0 NoCompressor, mode 1 snappy header pass
-hipError_t launch_decode_dma(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                             int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
 // bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
 // the shift tables it reads (Launch::stab) are built on the host once per context
 size_t stream_tab_words();

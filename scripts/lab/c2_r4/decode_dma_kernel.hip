@@ -1,4 +1,7 @@
-// bhg_decode_dma.hip -- the record decode as an LDS-DMA stream (gfx950).
+// decode_dma_kernel.hip -- LAB (not product code; included by dma_lab.hip): the record decode
+// as an LDS-DMA stream (gfx950).  Bit-exact against the product on the C2 batch, but 0.59-0.62 ms
+// against the register-staged k_decode_tile's 0.25-0.27 on the same boxes (its no-CRC floor:
+// 0.40-0.47 ms), so the product keeps k_decode_tile (profiles/r4/).
 //
 // k_decode_dma: readRecord + readKV + FNV-1 + masked CRC-32C (bithash/block2.go:31-66,
 // compress.go:57-59, internal/hash/fnv.go:19-23, internal/crc/crc.go:19-33) for a batch of
@@ -27,9 +30,9 @@
 // global memory by its 16 lanes in the same window structure ("global mode"; correct for any
 // length, slower).  CRC tables: CrcR8 (32 KiB, conflict free) + six 4-KiB shift tables, so the
 // ring (8 waves x 3 x 4,416 B) fits beside them in one 160-KiB workgroup per CU.
-#include "bhg_crc_tables.h"
-#include "bhg_device.h"
-#include "bhg_internal.h"
+#include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
+#include "../../../bitalosdb_amd/csrc/bhg_device.h"
+#include "../../../bitalosdb_amd/csrc/bhg_internal.h"
 
 namespace bhg {
 
@@ -122,11 +125,8 @@ __global__ __launch_bounds__(64 * DNW) void k_decode_dma(const uint8_t *__restri
     const uint32_t tb = lds_addr(lds_all), zb = tb + CrcR8::kBytes, rb = zb + DNZ * 4096;
     CrcR8::fill(tb);
     {
-        const uint32_t zsrc[DNZ] = {XZ32, XZ68, XZ136, XZ272, XZ544, XZ1088};
-#pragma unroll
-        for (uint32_t z = 0; z < DNZ; z++)
-            for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x)
-                lds_all[CrcR8::kBytes / 4 + 1024 * z + t] = xtab[1024 * zsrc[z] + t];
+        // xtab: the lab's Z_32, Z_68, Z_136, Z_272, Z_544, Z_1088 (1024 words each, this order)
+        for (uint32_t t = threadIdx.x; t < DNZ * 1024; t += blockDim.x) lds_all[CrcR8::kBytes / 4 + t] = xtab[t];
     }
     __syncthreads();
     const CrcR8 crc(tb);
@@ -152,15 +152,22 @@ __global__ __launch_bounds__(64 * DNW) void k_decode_dma(const uint8_t *__restri
     };
     auto ginfo = [&](uint32_t g, bool want_ec) {
         GInfo q;
+        // every scalar load of the group first (index clamped into the range), then one lgkmcnt wait
+        // -- loads interleaved with each record's checks were waited for record by record
+        bhg_handle hh[DG];
+        uint32_t ee[DG];
 #pragma unroll
         for (uint32_t r = 0; r < DG; r++) {
             const uint32_t i = DG * g + r;
-            bhg_handle h = {0, 0, 0};
-            uint32_t e = 0;
-            if (i < cnt) {
-                h = handles[r0 + i];
-                if (want_ec && expected_crc != nullptr) e = expected_crc[r0 + i];
-            }
+            const uint32_t ic = r0 + (i < cnt ? i : (cnt ? cnt - 1 : 0u));
+            hh[r] = handles[ic];
+            ee[r] = (want_ec && expected_crc != nullptr) ? expected_crc[ic] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < DG; r++) {
+            const uint32_t i = DG * g + r;
+            const bhg_handle h = i < cnt ? hh[r] : bhg_handle{0, 0, 0};
+            const uint32_t e = i < cnt ? ee[r] : 0u;
             uint32_t st = BHG_ST_OK, L = 0;
             if (i >= cnt) st = 0xffffffffu;
             else if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;                                      // reader.go:234-236

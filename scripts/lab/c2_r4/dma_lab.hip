@@ -30,7 +30,7 @@
 #include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
 #include "../../../bitalosdb_amd/csrc/bhg_device.h"
 #include "../../../include/bithashgpu.h"
-#include "../../../bitalosdb_amd/csrc/bhg_decode_dma.hip"  // the product kernels, timed beside the lab one
+#include "decode_dma_kernel.hip"  // the product-shaped DMA kernel (lab), timed beside the product tile kernel
 #include "../../../bitalosdb_amd/csrc/bhg_decode_tile.hip"
 
 #define CK(x)                                                                                  \
@@ -175,19 +175,26 @@ __global__ __launch_bounds__(64 * NW) void k_decode_dma(const uint8_t *__restric
     };
     auto ginfo = [&](uint32_t g, bool want_ec) {
         GInfo q;
+        // every scalar load of the group first (index clamped into the range), then one lgkmcnt wait
+        // -- loads interleaved with each record's checks were waited for record by record
+        bhg_handle hh[G];
+        uint32_t ee[G];
 #pragma unroll
         for (uint32_t r = 0; r < G; r++) {
             const uint32_t i = G * g + r;
-            bhg_handle h = {0, 0, 0};
-            uint32_t e = 0;
-            if (i < cnt) {
-                h = handles[r0 + i];
-                if (want_ec && expected_crc != nullptr) e = expected_crc[r0 + i];
-            }
+            const uint32_t ic = r0 + (i < cnt ? i : (cnt ? cnt - 1 : 0u));
+            hh[r] = handles[ic];
+            ee[r] = (want_ec && expected_crc != nullptr) ? expected_crc[ic] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < G; r++) {
+            const uint32_t i = G * g + r;
+            const bhg_handle h = i < cnt ? hh[r] : bhg_handle{0, 0, 0};
+            const uint32_t e = i < cnt ? ee[r] : 0u;
             uint32_t st = BHG_ST_OK, L = 0;
-            if (i >= cnt) st = 0xffffffffu;  // no record
-            else if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;
-            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;
+            if (i >= cnt) st = 0xffffffffu;
+            else if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;                                      // reader.go:234-236
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) st = BHG_ST_INCOMPLETE;  // :251-258
             else L = h.length;
             q.a[r] = base + h.offset;
             q.L[r] = L;
@@ -438,7 +445,7 @@ static void launch_tile(const uint8_t *src, uint64_t len, const bhg_handle *h, u
     const uint64_t tiles = (n + 63) / 64;
     uint64_t need = (tiles + 7) / 8;
     uint32_t grid = (uint32_t)(need < (uint64_t)cus ? need : cus);
-    hipLaunchKernelGGL((bhg::k_decode_tile<8, 2, BAL>), dim3(grid), dim3(512), 0, s, src, len, h, n, ec, out, g_ztab);
+    hipLaunchKernelGGL((bhg::k_decode_tile<8, 2>), dim3(grid), dim3(512), 0, s, src, len, h, n, ec, out, g_ztab);
 }
 
 int main(int argc, char **argv) {
@@ -485,8 +492,9 @@ int main(int argc, char **argv) {
     struct V { const char *name; lfn fn; };
     static uint32_t *xt = nullptr;
     if (!xt) {
-        std::vector<uint32_t> x(1024u * XTAB_N);
-        build_xtab(x.data());
+        std::vector<uint32_t> x(1024u * 6);
+        const uint64_t zl[6] = {32, 68, 136, 272, 544, 1088};
+        for (int k = 0; k < 6; k++) crc32c_shift_table(zl[k], x.data() + 1024 * k);
         CK(hipMalloc(&xt, x.size() * 4));
         CK(hipMemcpy(xt, x.data(), x.size() * 4, hipMemcpyHostToDevice));
     }
@@ -497,8 +505,7 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&g_ztab, zt.size() * 4));
         CK(hipMemcpy(g_ztab, zt.data(), zt.size() * 4, hipMemcpyHostToDevice));
     }
-    const V vs[] = {{"tile_bal0", launch_tile<0>}, {"tile_bal1", launch_tile<1>}, {"tile_bal0_again", launch_tile<0>},
-                    {"tile_bal1_again", launch_tile<1>},{"dma_w8_d3_pf", launch<8, 3>},
+    const V vs[] = {{"tile", launch_tile<0>}, {"product_dma", launch_product},{"dma_w8_d3_pf", launch<8, 3>},
                     {"floor_w8_nocrc", launch<8, 3, 0>}};
     auto prod = [&]() { if (bhg_decode_batch(ctx, src, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
     for (int it = 0; it < 200; it++) prod();  // clocks
