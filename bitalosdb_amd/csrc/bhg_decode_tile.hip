@@ -32,6 +32,14 @@
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
+#ifndef BHG_TILE_PF
+// bit 0 / bit 1: the next tile's head words 0..15 / round-0 windows loaded in round 7 of the
+// current tile.  Measured on the C2 layout (profiles/r4/pf_lab_tile_prefetch.txt, medians of
+// 2 x 60): PF 0 / 1 / 2 / 3 = 0.254 / 0.366 / 0.251 / 0.346 ms -- bit 1 reuses the free window
+// buffer (189 VGPRs), bit 0 keeps 16 more words live across the loop and spills (256 + scratch).
+#define BHG_TILE_PF 2
+#endif
+
 #ifndef BHG_TILE_NCH
 #define BHG_TILE_NCH 2  // measured: 1 / 2 / 4 chains 0.2455 / 0.2413 / 0.2445 ms (scripts/lab/run_tilevar.sh)
 #endif
@@ -54,7 +62,7 @@ __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
 // NCH: interleaved CRC chains per 128-B window (1, 2 or 4), folded with Z_{128/NCH}.  With
 // 2 waves per SIMD and a round's loads in flight, one chain's 32 dependent steps hide behind
 // memory; every fold costs a conflicted shift-table lookup.
-template <int WPB, int NCH>
+template <int WPB, int NCH, int PF>
 __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restrict__ src, uint64_t src_len,
                                                           const bhg_handle *__restrict__ handles, uint32_t n,
                                                           const uint32_t *__restrict__ expected_crc,
@@ -84,89 +92,126 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     bhg_handle hn = {0, 0, 0};
     if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    // a record's geometry from its handle: Reader.readData's checks (reader.go:234-258), the
+    // window count m = ceil(L / 128) and the head length hl = L - 128 (m-1) in 1..128
+    struct Geo {
+        uint64_t p;
+        uint32_t st, L, m, hl;
+        bool inb;
+    };
+    auto geo = [&](const bhg_handle &h, bool valid) {
+        Geo g;
+        g.st = BHG_ST_OK;
+        g.inb = false;
+        if (valid) {
+            if (h.length == 0) g.st = BHG_ST_ILLEGAL_LENGTH;                  // reader.go:234-236
+            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset)
+                g.st = BHG_ST_INCOMPLETE;                                     // reader.go:251-258
+            else g.inb = true;
+        }
+        g.L = g.inb ? h.length : 0u;
+        g.p = base + h.offset;
+        g.m = g.inb ? (g.L + 127) / 128 : 1u;
+        g.hl = g.L - 128 * (g.m - 1);
+        return g;
+    };
+    // the record head [p & ~3, +132): words 0..15, then 16..32 when hl > 60
+    auto load_head_lo = [&](uint32_t *hw, const Geo &g) {
+        const uint64_t ha = g.p & ~3ull;
+        if (!g.inb) return;
+        if (ha + 132 <= end) {
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+        }
+    };
+    auto load_head_hi = [&](uint32_t *hw, const Geo &g) {
+        const uint64_t ha = g.p & ~3ull;
+        if (!g.inb) return;
+        if (g.hl > 60) {
+            if (ha + 132 <= end) {
+#pragma unroll
+                for (int t = 4; t < 8; t++) {
+                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
+                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
+                }
+                hw[32] = gld<uint32_t>(ha + 128);
+            } else {
+#pragma unroll
+                for (int t = 16; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
+            }
+        } else {
+#pragma unroll
+            for (int t = 16; t < 33; t++) hw[t] = 0;
+        }
+    };
+    // round s's window plan for lane (rr, j): record 8s + rr of the tile whose geometry the lanes hold
+    auto rinfo = [&](uint32_t s, const Geo &g, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
+        const uint32_t sl = 8 * s + rr;
+        const uint32_t Lr = __shfl(g.L, sl, 64);
+        const uint64_t pr = shfl_u64(g.p, sl);
+        mm = __shfl(g.m, sl, 64);
+        wb = pr + (Lr - 128 * (mm - 1));  // start of window 1
+        q0 = (int32_t)(mm - 1) - (int32_t)j;
+        hasw = Lr != 0 && q0 >= 1;
+        qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
+    };
+    auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
+        const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
+        if (a + 132 <= end) {
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                const u32x4 x = gld<u32x4_a4>(a + 16 * t);
+                w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
+            }
+            w[32] = gld<uint32_t>(a + 128);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
+        }
+    };
+    uint32_t hw[33];
+    uint32_t fw[2][33];
+    uint64_t wb = 0;
+    uint32_t mm = 1;
+    int32_t qf = 0, q0 = 0;
+    bool hasw = false;
+    if (PF != 0 && tile < ntiles) {  // the first tile's prefetched part; later tiles' come from round 7
+        const Geo g0 = geo(hn, tile * 64 + lane < n);
+        if (PF & 1) load_head_lo(hw, g0);
+        if (PF & 2) {
+            rinfo(0, g0, wb, mm, qf, q0, hasw);
+            if (hasw) load_win(fw[0], wb, qf);
+        }
+    }
     for (; tile < ntiles; tile += tstride) {
         // ---------------- phase 1: lane = record (Reader.readData's checks, readRecord, readKV)
         const bhg_handle h = hn;
         const uint32_t i = tile * 64 + lane;
-        {
-            const uint32_t tn = tile + tstride;
-            if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
-        }
+        const uint32_t tn = tile + tstride;
+        if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
         const bool valid = i < n;
         // requested here, used after phase 2: a load issued at the end would expose its latency per tile
         const uint32_t ecrc = (expected_crc != nullptr && valid) ? expected_crc[i] : 0u;
-        uint32_t st = BHG_ST_OK;
-        bool inb = false;
-        if (valid) {
-            if (h.length == 0) st = BHG_ST_ILLEGAL_LENGTH;                    // reader.go:234-236
-            else if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset)
-                st = BHG_ST_INCOMPLETE;                                       // reader.go:251-258
-            else inb = true;
-        }
-        const uint32_t L = inb ? h.length : 0u;
-        const uint64_t p = base + h.offset;
-        const uint32_t m = inb ? (L + 127) / 128 : 1u;
-        const uint32_t hl = L - 128 * (m - 1);
-        uint32_t hw[33];
-        const uint64_t ha = p & ~3ull;
+        const Geo g = geo(h, valid);
+        const uint32_t st = g.st, L = g.L, m = g.m, hl = g.hl;
+        const uint64_t p = g.p;
+        const bool inb = g.inb;
         const uint32_t hsh = (uint32_t)(p & 3);
-        if (inb) {
-            if (ha + 132 <= end) {
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
-                    hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
-                }
-                if (hl > 60) {
-#pragma unroll
-                    for (int t = 4; t < 8; t++) {
-                        const u32x4 v = gld<u32x4_a4>(ha + 16 * t);
-                        hw[4 * t] = v.x; hw[4 * t + 1] = v.y; hw[4 * t + 2] = v.z; hw[4 * t + 3] = v.w;
-                    }
-                    hw[32] = gld<uint32_t>(ha + 128);
-                } else {
-#pragma unroll
-                    for (int t = 16; t < 33; t++) hw[t] = 0;
-                }
-            } else {
-#pragma unroll
-                for (int t = 0; t < 33; t++) hw[t] = ld32_safe(ha + 4 * t, end);
-            }
-        }
-        // ---------------- phase 2 state; round 0's windows are requested here, before phase 1's
-        // CRC / FNV-1 work, so that work overlaps their memory latency
         uint32_t mycrc = 0;
-        uint32_t fw[2][33];
-        auto rinfo = [&](uint32_t s, uint64_t &wb, uint32_t &mm, int32_t &qf, int32_t &q0, bool &hasw) {
-            const uint32_t sl = 8 * s + rr;
-            const uint32_t Lr = __shfl(L, sl, 64);
-            const uint64_t pr = shfl_u64(p, sl);
-            mm = __shfl(m, sl, 64);
-            wb = pr + (Lr - 128 * (mm - 1));  // start of window 1
-            q0 = (int32_t)(mm - 1) - (int32_t)j;
-            hasw = Lr != 0 && q0 >= 1;
-            qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
-        };
-        auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
-            const uint64_t a = (wb + 128ull * (uint32_t)(q - 1)) & ~3ull;
-            if (a + 132 <= end) {
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    const u32x4 x = gld<u32x4_a4>(a + 16 * t);
-                    w[4 * t] = x.x; w[4 * t + 1] = x.y; w[4 * t + 2] = x.z; w[4 * t + 3] = x.w;
-                }
-                w[32] = gld<uint32_t>(a + 128);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 33; t++) w[t] = ld32_safe(a + 4 * t, end);
-            }
-        };
-        uint64_t wb;
-        uint32_t mm;
-        int32_t qf, q0;
-        bool hasw;
-        rinfo(0, wb, mm, qf, q0, hasw);
-        if (hasw) load_win(fw[0], wb, qf);
+        if (!(PF & 1)) load_head_lo(hw, g);
+        load_head_hi(hw, g);
+        if (!(PF & 2)) {
+            // round 0's windows are requested here, before phase 1's CRC / FNV-1 work, so that
+            // work overlaps their memory latency
+            rinfo(0, g, wb, mm, qf, q0, hasw);
+            if (hasw) load_win(fw[0], wb, qf);
+        }
         uint32_t hcrc = 0xffffffffu;  // crc.New: Go's crc32.Update starts from ^0
         uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
         uint64_t trailer = 255;       // InternalKeyKindInvalid when ikeySize < 8
@@ -233,8 +278,17 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             const int32_t qf_c = qf, q0_c = q0;
             const bool hasw_c = hasw;
             if (s + 1 < 8) {
-                rinfo(s + 1, wb, mm, qf, q0, hasw);
+                rinfo(s + 1, g, wb, mm, qf, q0, hasw);
                 if (hasw) load_win(fw[cb ^ 1], wb, qf);
+            } else if (PF != 0 && tn < ntiles) {
+                // the next tile's record heads (into hw, dead since phase 1) and / or its round-0
+                // windows (into the free buffer), in flight across this round and the stores
+                const Geo gn = geo(hn, tn * 64 + lane < n);
+                if (PF & 1) load_head_lo(hw, gn);
+                if (PF & 2) {
+                    rinfo(0, gn, wb, mm, qf, q0, hasw);
+                    if (hasw) load_win(fw[cb ^ 1], wb, qf);
+                }
             }
             const uint32_t hc = __shfl(hz, 8 * s + rr, 64);
             uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
@@ -280,7 +334,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);  // record 8s + r sits on lane 8r
             if ((lane >> 3) == s) mycrc = got;
         }
-        wait_loads_done();  // unconditional: see bhg_device.h
+        if (PF == 0) wait_loads_done();  // unconditional: see bhg_device.h
         if (valid) {
             uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
             uint64_t dtr = 0;
@@ -315,7 +369,7 @@ hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_
     uint64_t cap = (uint64_t)L.num_cus;  // 148 KiB of LDS: one workgroup per CU
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_tile<WPB, BHG_TILE_NCH>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
+    hipLaunchKernelGGL((k_decode_tile<WPB, BHG_TILE_NCH, BHG_TILE_PF>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
                        expected_crc, out, L.ztab);
     return hipGetLastError();
 }
