@@ -69,3 +69,31 @@ def test_no_selectable_kernel_variants():
     for k in ("k_diag", "k_decode_lane", "k_decode_coop", "k_decode_lanebuf", "k_snappy_wave", "k_decode_tile2"):
         assert k not in syms, k
     assert not re.search(rb"BHG_[A-Z_]*VARIANT", blob)
+
+
+def _src_default(fname, knob):
+    src = open(os.path.join(os.path.dirname(B.LIB_PATH), "..", "csrc", fname)).read()
+    m = re.search(r"#define %s (\d+)" % knob, src)
+    assert m, (fname, knob)
+    return int(m.group(1))
+
+
+def test_shipped_library_has_default_knobs():
+    """The .so was built with the sources' default compile knobs: each templated kernel exists
+    in exactly the instantiation its file's #define defaults select (a lab build with -D knobs
+    would ship a different one)."""
+    B.build()
+    blob = open(B.LIB_PATH, "rb").read()
+    pf = _src_default("bhg_decode_tile.hip", "BHG_TILE_PF")
+    nch = _src_default("bhg_decode_tile.hip", "BHG_TILE_NCH")
+    bpw = _src_default("bhg_snappy_dec.hip", "BHG_SL_BPW")
+    slot = _src_default("bhg_snappy_dec.hip", "BHG_SL_SLOT")
+    want = {
+        rb"_ZN3bhg13k_decode_tileI": b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf),
+        rb"_ZN3bhg12k_snappy_ldsI": b"_ZN3bhg12k_snappy_ldsILi%dELi%dEE" % (bpw, slot),
+    }
+    for prefix, name in want.items():
+        found = set(re.findall(re.escape(prefix) + rb"[A-Za-z0-9]+?EE", blob))
+        assert found == {name}, (prefix, found, name)
+    enc = set(re.findall(rb"_ZN3bhg12k_snappy_encI[A-Za-z0-9]+?EE", blob))
+    assert enc == {b"_ZN3bhg12k_snappy_encILi2048ELi1ELi4EE", b"_ZN3bhg12k_snappy_encILi4096ELi3ELi3EE"}, enc
