@@ -318,7 +318,7 @@ __device__ __forceinline__ SlInfo sl_finish(const SlRaw &w, uint32_t n, uint64_t
     else if (w.o1 > out_cap || w.o1 - w.o0 < w.dlen)
         r.mode = SL_TOOLARGE;
     else
-        r.mode = (w.dlen <= 1024u && r.clen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
+        r.mode = (w.dlen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
     return r;
 }
 
@@ -449,6 +449,17 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
                 c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
             }
             if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 16 * lane) = c;
+        }
+        // streams past 64 chunks (1,025 .. SLOT - 24 B: values snappy could not shrink, ~1 in
+        // 3,000 dict values): the rest loaded here, synchronously -- rare, and it keeps them
+        // out of the global-memory pass
+        for (uint64_t lm = __ballot(cur.mode == SL_LDS && cur.clen > 1024u); lm; lm &= lm - 1) {
+            const int b = __builtin_ctzll(lm);
+            const uint32_t clb = __builtin_amdgcn_readlane(cur.clen, b);
+            if (1024u + 16 * lane < clb) {
+                const u32x4 c = ld16_hi(readlane_u64(cur.cp, b) + 1024u + 16 * lane, end);
+                *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 1024u + 16 * lane) = c;
+            }
         }
         sl_wsync();
         // 2. descriptors of the group after next, then the next group's streams in flight

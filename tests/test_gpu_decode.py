@@ -242,6 +242,47 @@ def test_snappy_inplace_spill_and_oversize(codec):
     assert gvals[int(goff[0]):int(goff[1])].tobytes() == want
 
 
+def _lit(data):
+    n = len(data)
+    if n <= 60:
+        return bytes([(n - 1) << 2]) + data
+    if n <= 256:
+        return bytes([60 << 2, n - 1]) + data
+    return bytes([61 << 2]) + (n - 1).to_bytes(2, "little") + data
+
+
+def test_snappy_long_streams_in_lds(codec):
+    """Streams longer than the 64 chunks a lane-per-chunk staging covers (1,025 .. 1,064 B
+    for a <= 1 KiB value: values snappy cannot shrink) are decoded in their LDS slot, the
+    bytes past 1 KiB loaded separately; longer ones still go to the global-memory pass.
+    k one-byte literals then one literal of the rest: stream = 1,028 + k bytes for 1,024 out.
+    The last record (the end of src) is one of the longest LDS-path streams."""
+    rng = random.Random(33)
+    streams = []
+    for i in range(1200):
+        k = rng.choice([0, 3, 10, 22, 28, 36, 40, 42, 60])
+        out = rand_bytes(rng, 1024)
+        st = _uvarint(1024) + b"".join(_lit(out[j:j + 1]) for j in range(k)) + _lit(out[k:])
+        assert O.snappy_decode(st) == out
+        streams.append(st)
+        if i % 5 == 0:
+            streams.append(O.snappy_encode(rand_bytes(rng, rng.choice([1000, 1010, 1024]))))
+    streams.append(_uvarint(1024) + b"".join(_lit(bytes([j])) for j in range(36)) + _lit(rand_bytes(rng, 988)))
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"long%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert (exp["status"] == 0).all()
+    assert np.array_equal(goff, eoff)
+    assert gvals.tobytes() == evals[:int(eoff[-1])].tobytes()
+
+
 def _view_with_bit31(nbytes, dev):
     """A uint8 device view of nbytes whose address has bit 31 of its low word set
     over its whole length (low word in [0x80000100, 0xFFFFFFFF])."""
