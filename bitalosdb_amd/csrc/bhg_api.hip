@@ -176,7 +176,7 @@ bhg_ctx *bhg_create(int device, int flags) {
              hipMemcpy(c->stab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
     if (ok) {
-        std::vector<uint32_t> z(1024u * bhg::XTAB_N);
+        std::vector<uint32_t> z(bhg::kXTabWords);
         bhg::build_xtab(z.data());
         ok = hipMalloc(reinterpret_cast<void **>(&c->xtab), z.size() * 4) == hipSuccess &&
              hipMemcpy(c->xtab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
@@ -597,7 +597,10 @@ int bhg_crc32c_masked_long(bhg_ctx *c, const uint8_t *src, uint64_t src_len, con
     if (n == 0) return BHG_OK;
     if (!handles || !out_crc || (!src && src_len)) { set_err(c, "null buffer"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
-    HIP_TRY(c, bhg::launch_crc_long(launch_of(c, stream), src, src_len, handles, n, out_crc));
+    bhg::Launch L = launch_of(c, stream);
+    Scratch sc;
+    if (int r = scratch_alloc(c, L.stream, bhg::crc_long_scratch_bytes(n), sc)) return r;
+    HIP_TRY(c, bhg::launch_crc_long(L, src, src_len, handles, n, out_crc, sc.base));
     return BHG_OK;
 }
 

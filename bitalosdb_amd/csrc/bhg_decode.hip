@@ -3,13 +3,14 @@
 //   k_crc_ranges / k_fnv_ranges   lane per range: crc.New(b).Value() and
 //                                 hash.Fnv32 (internal/crc/crc.go:23-33,
 //                                 internal/hash/fnv.go:19-23)
-//   k_crc_long                    workgroup per LONG range (the per-table
-//                                 indexhash_checksum, writer.go:476-478)
+//   k_crc_long_part / _join       LONG ranges, up to 64 workgroups each (the
+//                                 per-table indexhash_checksum, writer.go:476-478)
 //   launch_decode                 NoCompressor: k_decode_tile
 //                                 (bhg_decode_tile.hip); snappy: the header /
 //                                 CRC pass of k_decode_stream
 //                                 (bhg_decode_stream.hip), then k_snappy_rt
 //                                 (bhg_snappy_dec.hip) after the size scan
+#include "bhg_crc_tables.h"
 #include "bhg_decode_stream.h"
 #include "bhg_device.h"
 #include "bhg_internal.h"
@@ -48,65 +49,100 @@ __global__ __launch_bounds__(256) void k_fnv_ranges(const uint8_t *__restrict__ 
     }
 }
 
-// k_crc_long: masked CRC-32C of a few LONG ranges -- the per-table
-// indexhash_checksum verify of SURVEY 8(a) A6(ii): writer.go:476-478 stores
-// crc.New(indexhash_data).Value() (internal/crc/crc.go:23-33) and a table open
-// re-computes it over ~1.5 MB.  k_crc_ranges gives a range one lane, which
-// walks 1.5 MB serially (~20 ms); here one workgroup takes a range:
-//   * the range is cut into kLongChunk-byte chunks aligned to its END; chunk 0
-//     holds the remainder (1..kLongChunk bytes) and runs from Go's initial
-//     state ^0, every other chunk from state 0; one lane per chunk;
-//   * lane 0 folds the chunk states in order, state = Z_4096(state) ^ crc0(chunk)
-//     (CRC linearity: crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B));
-//   * Z_4096 is built in LDS from the context's Z_1024 table (four applications
-//     per entry); chunks are taken kLongPass at a time, the state carried over.
-constexpr uint32_t kLongChunk = 4096, kLongPass = 2048, kLongThreads = 512;
+// k_crc_long_part + k_crc_long_join: masked CRC-32C of LONG ranges -- the per-table
+// indexhash_checksum of SURVEY 8(a) A6(ii): writer.go:476-478 stores
+// crc.New(indexhash_data).Value() (internal/crc/crc.go:23-33); a table open re-computes it,
+// and the table tail (bhg_tail.hip) writes it.  A range is cut into 64 x 256 spans of
+// 2^(10+s) bytes aligned to its END (s the smallest with 64 x 256 x 2^(10+s) >= its length),
+// so every span is full except the first non-empty one, which starts at byte 0 and runs from
+// Go's initial state ^0; every other span runs from state 0.  A lane CRCs one span; then, by
+// CRC linearity over GF(2),
+//     crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B),
+// a workgroup (one of 64 parts) folds its 256 span states as a tree whose right subtrees are
+// always full (level l shifts by Z_{2^l spans}), and one wave per range folds the 64 part
+// states the same way (Z_{2^(8+l) spans}).  Empty spans left of the first hold 0, and Z(0) = 0.
+// The shift tables Z_{2^(10+j)} come from the context (bhg_crc_tables.h kXLong).  Round 3's
+// one-workgroup-per-range kernel took ~0.6 ms for a 10-MB index (one CU); this spreads a range
+// over up to 64 workgroups.
+constexpr uint32_t kLongParts = 64, kLongThreads = 256;
 
 __device__ __forceinline__ uint32_t zapply_tab(const uint32_t *Zt, uint32_t c) {
     return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
 }
 
-__global__ __launch_bounds__(kLongThreads) void k_crc_long(const uint8_t *__restrict__ src, uint64_t src_len,
-                                                           const bhg_handle *__restrict__ handles, uint32_t n,
-                                                           uint32_t *__restrict__ out, const uint32_t *__restrict__ gz1024) {
-    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<8>::kWords];
-    __shared__ uint32_t Z1[1024], Z[1024], C[kLongPass];
-    Crc4Lds<8>::fill(T);
-    for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x) Z1[t] = gz1024[t];
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x) {
-        uint32_t x = (t & 255u) << (8 * (t >> 8));  // S[k][i] = Z_4096(i << 8k)
-#pragma unroll
-        for (int r = 0; r < 4; r++) x = zapply_tab(Z1, x);
-        Z[t] = x;
+// the range's span exponent s and span count (spans of 2^(10+s) bytes covering len)
+__device__ __forceinline__ void long_geo(uint64_t len, uint32_t &s, uint64_t &nspan) {
+    s = 0;
+    while (((uint64_t)kLongParts * kLongThreads << (10 + s)) < len) s++;
+    nspan = (len + (1ull << (10 + s)) - 1) >> (10 + s);
+}
+
+__global__ __launch_bounds__(kLongThreads) void k_crc_long_part(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                                const bhg_handle *__restrict__ handles,
+                                                                uint32_t *__restrict__ part,
+                                                                const uint32_t *__restrict__ zl) {
+    const uint32_t i = blockIdx.y, p = blockIdx.x, t = threadIdx.x;
+    const bhg_handle h = handles[i];
+    const bool ok = h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
+    const uint64_t len = ok ? h.length : 0;
+    uint32_t s;
+    uint64_t nspan;
+    long_geo(len, s, nspan);
+    const uint64_t first = (uint64_t)kLongParts * kLongThreads - nspan;  // global index of the first non-empty span
+    if ((uint64_t)(p + 1) * kLongThreads <= first) {                    // an empty part (whole workgroup)
+        if (t == 0) part[(uint64_t)i * kLongParts + p] = 0;
+        return;
     }
+    __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<8>::kWords];
+    __shared__ uint32_t Z[8 * 1024], st[kLongThreads];
+    Crc4Lds<8>::fill(T);
+    for (uint32_t w = t; w < 8 * 1024; w += kLongThreads) Z[w] = zl[(uint64_t)s * 1024 + w];  // Z_{span 2^l}, l = 0..7
     __syncthreads();
     const Crc4Lds<8> crc(T);
-    const uint64_t base = (uint64_t)src, end = base + src_len;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const bhg_handle h = handles[i];
-        if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset) {  // as k_crc_ranges: 0
-            if (threadIdx.x == 0) out[i] = 0;
-            continue;
-        }
-        const uint64_t len = h.length, p = base + h.offset;
-        const uint64_t nch = len ? (len + kLongChunk - 1) / kLongChunk : 0;
-        const uint64_t t0 = len - (uint64_t)kLongChunk * (nch ? nch - 1 : 0);  // chunk 0 length
-        uint32_t state = 0xffffffffu;  // crc.New: Go starts from ^0
-        for (uint64_t k0 = 0; k0 < nch; k0 += kLongPass) {
-            const uint64_t kend = nch - k0 < kLongPass ? nch : k0 + kLongPass;
-            for (uint64_t k = k0 + threadIdx.x; k < kend; k += blockDim.x) {
-                const uint64_t a = k == 0 ? p : p + t0 + (uint64_t)kLongChunk * (k - 1);
-                C[k - k0] = crc_range(crc, k == 0 ? 0xffffffffu : 0u, a, k == 0 ? t0 : kLongChunk, end);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0)
-                for (uint64_t k = k0; k < kend; k++) state = k == 0 ? C[0] : zapply_tab(Z, state) ^ C[k - k0];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[i] = crc_mask(~state);  // crc.go:31-33
+    const uint64_t g = (uint64_t)p * kLongThreads + t;
+    uint32_t c = 0;
+    if (g >= first) {
+        const uint64_t span = 1ull << (10 + s), k = g - first;  // k: span index from the range start
+        const uint64_t e = len - (nspan - 1 - k) * span;       // end of the span (exclusive)
+        const uint64_t b = k == 0 ? 0 : e - span;
+        c = crc_range(crc, k == 0 ? 0xffffffffu : 0u, (uint64_t)src + h.offset + b, e - b, (uint64_t)src + src_len);
+    }
+    st[t] = c;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t l = 0; l < 8; l++) {
+        const uint32_t w = 1u << l;
+        if ((t & (2 * w - 1)) == 2 * w - 1) st[t] = zapply_tab(Z + l * 1024, st[t - w]) ^ st[t];
+        __syncthreads();
+    }
+    if (t == kLongThreads - 1) part[(uint64_t)i * kLongParts + p] = st[t];
+}
+
+// one wave per range: lane = part
+__global__ __launch_bounds__(64) void k_crc_long_join(uint64_t src_len, const bhg_handle *__restrict__ handles,
+                                                      const uint32_t *__restrict__ part, const uint32_t *__restrict__ zl,
+                                                      uint32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    const bhg_handle h = handles[i];
+    const bool ok = h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
+    const uint64_t len = ok ? h.length : 0;
+    uint32_t s;
+    uint64_t nspan;
+    long_geo(len, s, nspan);
+    uint32_t v = part[(uint64_t)i * kLongParts + lane];
+#pragma unroll
+    for (uint32_t l = 0; l < 6; l++) {
+        const uint32_t w = 1u << l;
+        const uint32_t left = __shfl(v, (int)(lane >= w ? lane - w : 0), 64);
+        if ((lane & (2 * w - 1)) == 2 * w - 1) v = zapply_tab(zl + (uint64_t)(s + 8 + l) * 1024, left) ^ v;
+    }
+    if (lane == 63) {
+        const uint32_t state = len ? v : 0xffffffffu;  // crc.New of nothing: ^0
+        out[i] = ok ? crc_mask(~state) : 0u;           // crc.go:31-33; out of bounds: 0, as k_crc_ranges
     }
 }
+
+size_t crc_long_scratch_bytes(uint32_t n) { return (size_t)n * kLongParts * 4; }
 
 // ---------------------------------------------------------------------------
 // host launchers
@@ -124,10 +160,17 @@ hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_l
 }
 
 hipError_t launch_crc_long(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           uint32_t *out) {
-    const uint32_t grid = n < 65535u ? n : 65535u;
-    hipLaunchKernelGGL(k_crc_long, dim3(grid), dim3(kLongThreads), 0, L.stream, src, src_len, h, n, out, L.ztab);
-    return hipGetLastError();
+                           uint32_t *out, void *scratch) {
+    uint32_t *part = reinterpret_cast<uint32_t *>(scratch);
+    const uint32_t *zl = L.xtab + kXLong;
+    for (uint32_t i0 = 0; i0 < n; i0 += 65535u) {  // gridDim.y <= 65535
+        const uint32_t m = n - i0 < 65535u ? n - i0 : 65535u;
+        hipLaunchKernelGGL(k_crc_long_part, dim3(kLongParts, m), dim3(kLongThreads), 0, L.stream, src, src_len, h + i0,
+                           part, zl);
+        hipLaunchKernelGGL(k_crc_long_join, dim3(m), dim3(64), 0, L.stream, src_len, h + i0, part, zl, out + i0);
+        if (hipError_t e = hipGetLastError()) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

@@ -68,8 +68,10 @@ inline size_t snappy_list_bytes(uint32_t n) { return 4 + 4 * (size_t)n; }
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)
+size_t crc_long_scratch_bytes(uint32_t n);
+// scratch: crc_long_scratch_bytes(n) bytes
 hipError_t launch_crc_long(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           uint32_t *out);
+                           uint32_t *out, void *scratch);
 hipError_t launch_fnv_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 

@@ -73,6 +73,10 @@ struct TailArgs {
     uint64_t *keep, *kpos;          // n+1
     uint64_t *kscan;                // n+1: exclusive scan of keep
     uint32_t *klist;                // n: kept positions, in sorted order
+    uint64_t *kpre, *kaddr;         // n: per kept entry (klist order): big-endian first 8 key bytes, key address
+    uint32_t *klen, *katk;          // n: ... key length, kat of its position
+    uint64_t *cpre, *caddr;         // n: the same per conflict entry (clist order)
+    uint32_t *cklen;                // n
     uint32_t *kat;                  // n: when updateHash last assigned conflictKeys[key] from this run
     uint32_t *clist, *cord;         // n
     uint64_t *csz;                  // n+1: conflict entry sizes -> offsets
@@ -109,6 +113,14 @@ __device__ __forceinline__ bool key_lt(uint64_t a, uint32_t al, uint64_t b, uint
         if (x != y) return x < y;
     }
     return al < bl;
+}
+
+// the first 8 key bytes, big-endian, zero-padded: keys whose prefixes differ compare as their
+// prefixes do (bytes.Compare); equal prefixes need the full compare
+__device__ __forceinline__ uint64_t key_prefix(uint64_t kp, uint32_t kl) {
+    uint64_t x = 0;
+    for (uint32_t k = 0; k < 8; k++) x = (x << 8) | (k < kl ? ld8(kp + k) : 0u);
+    return x;
 }
 
 // byte j of the internal key userKey || trailer(seq 1, kind SET) (MakeInternalKey(k, 1, InternalKeyKindSet))
@@ -243,10 +255,20 @@ __global__ __launch_bounds__(256) void k_tail_keep(TailArgs a) {
     }
 }
 
-// kept positions, compacted: klist[kscan[j]] = j (kscan = exclusive scan of keep)
+// kept positions, compacted: klist[kscan[j]] = j (kscan = exclusive scan of keep), with each
+// kept key's prefix / address / length / kat laid out in the same order for k_tail_dedupe
 __global__ __launch_bounds__(256) void k_tail_klist(TailArgs a) {
     GRID_LOOP(j, a.n) {
-        if (a.kscan[j + 1] != a.kscan[j]) a.klist[a.kscan[j]] = (uint32_t)j;
+        if (a.kscan[j + 1] != a.kscan[j]) {
+            const uint64_t g = a.kscan[j];
+            uint64_t kp; uint32_t kl;
+            rec_key(a, a.idx_s[j], kp, kl);
+            a.klist[g] = (uint32_t)j;
+            a.kpre[g] = key_prefix(kp, kl);
+            a.kaddr[g] = kp;
+            a.klen[g] = kl;
+            a.katk[g] = a.kat[j];
+        }
     }
 }
 
@@ -254,7 +276,8 @@ __global__ __launch_bounds__(256) void k_tail_klist(TailArgs a) {
 // values for one key, possible through AddIkey) keeps the run that assigned it last.  Without
 // this the conflict list would hold a key twice and the rank permutation would break.  Each
 // kept position compares itself with the kept positions of its own table only (klist, sorted
-// by table like sk_s): O(kept_t^2) per table, not O(kept_t x records_t).
+// by table like sk_s): O(kept_t^2) per table, over the contiguous prefix / length arrays (the
+// key bytes only when both match).
 __global__ __launch_bounds__(256) void k_tail_dedupe(TailArgs a) {
     const uint32_t K = (uint32_t)a.kscan[a.n];
     GRID_LOOP(j, a.n) {
@@ -263,15 +286,14 @@ __global__ __launch_bounds__(256) void k_tail_dedupe(TailArgs a) {
             const uint64_t t = a.sk_s[j] >> 32;
             const uint32_t g0 = lower_bound(0, K, t << 32, [&](uint32_t g) { return a.sk_s[a.klist[g]]; });
             const uint32_t g1 = lower_bound(g0, K, (t + 1) << 32, [&](uint32_t g) { return a.sk_s[a.klist[g]]; });
-            uint64_t kp; uint32_t kl;
-            rec_key(a, a.idx_s[j], kp, kl);
-            const uint32_t at = a.kat[j];
+            const uint64_t gj = a.kscan[j];
+            const uint64_t pre = a.kpre[gj], kp = a.kaddr[gj];
+            const uint32_t kl = a.klen[gj], at = a.kat[j];
             for (uint32_t g = g0; g < g1 && f; g++) {
-                const uint32_t q = a.klist[g];
-                if (q == j || a.kat[q] < at || (a.kat[q] == at && q < j)) continue;
-                uint64_t kq; uint32_t lq;
-                rec_key(a, a.idx_s[q], kq, lq);
-                if (key_eq(kp, kl, kq, lq)) f = 0;
+                if (a.kpre[g] != pre || a.klen[g] != kl || g == gj) continue;
+                const uint32_t q = a.klist[g], aq = a.katk[g];
+                if (aq < at || (aq == at && q < j)) continue;
+                if (key_eq(kp, kl, a.kaddr[g], kl)) f = 0;
             }
         }
         a.kpos[j] = f;
@@ -280,7 +302,13 @@ __global__ __launch_bounds__(256) void k_tail_dedupe(TailArgs a) {
 
 __global__ __launch_bounds__(256) void k_tail_clist(TailArgs a) {
     GRID_LOOP(j, a.n) {
-        if (a.kpos[j + 1] != a.kpos[j]) a.clist[a.kpos[j]] = (uint32_t)j;
+        if (a.kpos[j + 1] != a.kpos[j]) {
+            const uint64_t f = a.kpos[j], g = a.kscan[j];
+            a.clist[f] = (uint32_t)j;
+            a.cpre[f] = a.kpre[g];
+            a.caddr[f] = a.kaddr[g];
+            a.cklen[f] = a.klen[g];
+        }
     }
 }
 
@@ -308,19 +336,20 @@ __device__ __forceinline__ uint32_t table_of_pos(const TailArgs &a, uint32_t j) 
 // tables whose tail slot ends past tail_cap are not written (tail_len 0)
 __device__ __forceinline__ bool tail_fits(const TailArgs &a, uint32_t t) { return a.tail_off[t + 1] <= a.tail_cap; }
 
-// lane per conflict key g: rank among its table's conflict keys by user key bytes (sort.Strings)
+// lane per conflict key g: rank among its table's conflict keys by user key bytes (sort.Strings),
+// over the contiguous prefix array (the key bytes only when two prefixes are equal)
 __global__ __launch_bounds__(256) void k_conf_rank(TailArgs a) {
     const uint32_t M = (uint32_t)a.kpos[a.n];
     GRID_LOOP(g, M) {
         const uint32_t t = table_of_pos(a, a.clist[g]);
         const uint32_t c0 = a.tab_c[t], c1 = a.tab_c[t + 1];
-        uint64_t kp; uint32_t kl;
-        rec_key(a, a.idx_s[a.clist[g]], kp, kl);
+        const uint64_t pre = a.cpre[g], kp = a.caddr[g];
+        const uint32_t kl = a.cklen[g];
         uint32_t rank = 0;
         for (uint32_t f = c0; f < c1; f++) {
-            uint64_t fp; uint32_t fl;
-            rec_key(a, a.idx_s[a.clist[f]], fp, fl);
-            rank += key_lt(fp, fl, kp, kl);
+            const uint64_t pf = a.cpre[f];
+            if (pf != pre) rank += pf < pre;
+            else if (f != g) rank += key_lt(a.caddr[f], a.cklen[f], kp, kl);
         }
         a.cord[c0 + rank] = (uint32_t)g;  // keys of a table are distinct (k_tail_dedupe): ranks are a permutation
     }
@@ -547,7 +576,8 @@ size_t tail_scratch_bytes(uint32_t n, uint32_t ntables) {
     const size_t N = (size_t)n + 1, T = (size_t)ntables + 1;
     return al(sort_tmp) + 2 * al(N * 8) + 2 * al(N * 4) + 2 * al(N * 8) + 2 * al(N * 4) + al(N * 8) + al(N) +
            3 * al(N * 8) + 2 * al(N * 4) + 2 * al(N * 4) + al(N * 8) + 2 * al(T * 4) + al(T * 8) + al(T * 8) +
-           al(T * 16) + al(T * 4) + al(scan_scratch_bytes(N > T ? N : T)) + 24 * 256;
+           al(T * 16) + al(T * 4) + al(scan_scratch_bytes(N > T ? N : T)) + al(crc_long_scratch_bytes((uint32_t)T)) +
+           4 * al(N * 8) + 3 * al(N * 4) + 32 * 256;
 }
 
 hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch) {
@@ -570,12 +600,16 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     a.run_key = (uint64_t *)take(N * 8); a.run_conf = take(N);
     a.keep = (uint64_t *)take(N * 8); a.kpos = (uint64_t *)take(N * 8); a.kat = (uint32_t *)take(N * 4);
     a.kscan = (uint64_t *)take(N * 8); a.klist = (uint32_t *)take(N * 4);
+    a.kpre = (uint64_t *)take(N * 8); a.kaddr = (uint64_t *)take(N * 8);
+    a.klen = (uint32_t *)take(N * 4); a.katk = (uint32_t *)take(N * 4);
+    a.cpre = (uint64_t *)take(N * 8); a.caddr = (uint64_t *)take(N * 8); a.cklen = (uint32_t *)take(N * 4);
     a.clist = (uint32_t *)take(N * 4); a.cord = (uint32_t *)take(N * 4);
     a.csz = (uint64_t *)take(N * 8);
     a.tab_run = (uint32_t *)take(TT * 4); a.tab_c = (uint32_t *)take(TT * 4);
     a.cbound = (uint64_t *)take(TT * 8); a.cinfo = (uint32_t *)take(TT * 8);
     a.crc_h = (bhg_handle *)take(TT * 16); a.crc = (uint32_t *)take(TT * 4);
     void *scan_s = take(scan_scratch_bytes(N > TT ? N : TT));  // also scans tail_off over the tables
+    void *crc_s = take(crc_long_scratch_bytes((uint32_t)TT));
 
     const uint32_t g = lane_grid(L, n ? n : 1, 256);
     e = hipMemsetAsync(a.cbound, 0, TT * 8, L.stream);
@@ -604,7 +638,7 @@ hipError_t launch_table_tail(const Launch &L, const TailLaunch &T, void *scratch
     hipLaunchKernelGGL(k_tail_shards, dim3(lane_grid(L, (uint64_t)nt * kShards, 256)), dim3(256), 0, L.stream, a);
     hipLaunchKernelGGL(k_tail_crch, dim3(lane_grid(L, nt, 256)), dim3(256), 0, L.stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_crc_long(L, T.tail, T.tail_cap, a.crc_h, nt, a.crc)) != hipSuccess) return e;
+    if ((e = launch_crc_long(L, T.tail, T.tail_cap, a.crc_h, nt, a.crc, crc_s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tail_finish, dim3((nt + 63) / 64), dim3(64), 0, L.stream, a);
     return hipGetLastError();
 }

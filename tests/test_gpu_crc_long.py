@@ -27,16 +27,17 @@ def codec():
 
 
 def test_long_ranges_match_restatement(codec):
-    """Chunk-boundary lengths (4 KiB chunks, 2048 chunks per pass), odd
-    alignments, a multi-pass range, empty and out-of-range handles."""
+    """Span-boundary lengths (1 KiB spans aligned to the range end, 64 x 256 of them before the
+    span doubles at 16 MiB), odd alignments, empty and out-of-range handles."""
     from bitalosdb_amd.codec import as_device_bytes, handles_tensor
     rng = np.random.default_rng(21)
     size = 20 << 20
     data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
     dsrc = as_device_bytes(data, codec.device)
     K = 4096
-    lens = [0, 1, 3, 4, 5, 63, 4095, K, K + 1, 2 * K - 1, 2 * K, 2 * K + 1, 1_510_000,
-            2048 * K - 1, 2048 * K, 2048 * K + 1, 17 << 20]
+    M16 = 16 << 20
+    lens = [0, 1, 3, 4, 5, 63, 1023, 1024, 1025, 4095, K, K + 1, 2 * K - 1, 2 * K, 2 * K + 1, 1_510_000,
+            2048 * K - 1, 2048 * K, 2048 * K + 1, M16 - 1, M16, M16 + 1, M16 + 1023, M16 + 1025, 17 << 20]
     hs = []
     for ln in lens:
         for off in (0, 1, 2, 3, 1001):
