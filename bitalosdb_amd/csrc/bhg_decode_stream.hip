@@ -5,18 +5,12 @@
 
 namespace bhg {
 
-#ifndef BHG_STREAM_NCH
-#define BHG_STREAM_NCH 4
-#endif
-#ifndef BHG_STREAM_WIN
-#define BHG_STREAM_WIN 128
-#endif
-#ifndef BHG_STREAM_PIPE
-#define BHG_STREAM_PIPE 0
-#endif
+constexpr int kStreamNch = 4;     // CRC chains per window
+constexpr int kStreamWin = 128;   // window bytes
+constexpr int kStreamPipe = 0;    // software-pipelined window loads (measured no faster)
 
 size_t stream_tab_words() { return kStreamTabWords; }
-void build_stream_tab_default(uint32_t *out) { build_stream_tab(out, BHG_STREAM_WIN, BHG_STREAM_NCH); }
+void build_stream_tab_default(uint32_t *out) { build_stream_tab(out, kStreamWin, kStreamNch); }
 
 // MODE 1 only: the NoCompressor decode is k_decode_tile (MODE 0 of this kernel measured
 // slower, DESIGN.md 4.1, and stays a lab build)
@@ -28,7 +22,7 @@ hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t sr
     const uint64_t need = (tiles + WPB - 1) / WPB, cap = (uint64_t)L.num_cus;
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_stream<1, BHG_STREAM_NCH, WPB, BHG_STREAM_WIN, BHG_STREAM_PIPE>), dim3(grid),
+    hipLaunchKernelGGL((k_decode_stream<1, kStreamNch, WPB, kStreamWin, kStreamPipe>), dim3(grid),
                        dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab);
     return hipGetLastError();
 }

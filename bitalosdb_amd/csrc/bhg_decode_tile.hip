@@ -32,17 +32,13 @@
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
-#ifndef BHG_TILE_PF
 // bit 0 / bit 1: the next tile's head words 0..15 / round-0 windows loaded in round 7 of the
 // current tile.  Measured on the C2 layout (profiles/r4/pf_lab_tile_prefetch.txt, medians of
 // 2 x 60): PF 0 / 1 / 2 / 3 = 0.254 / 0.366 / 0.251 / 0.346 ms -- bit 1 reuses the free window
 // buffer (189 VGPRs), bit 0 keeps 16 more words live across the loop and spills (256 + scratch).
-#define BHG_TILE_PF 2
-#endif
+constexpr int kTilePf = 2;
 
-#ifndef BHG_TILE_NCH
-#define BHG_TILE_NCH 2  // measured: 1 / 2 / 4 chains 0.2455 / 0.2413 / 0.2445 ms (scripts/lab/run_tilevar.sh)
-#endif
+constexpr int kTileNch = 2;  // CRC chains per window, measured: 1 / 2 / 4 chains 0.2455 / 0.2413 / 0.2445 ms (scripts/lab/run_tilevar.sh)
 
 namespace bhg {
 
@@ -369,7 +365,7 @@ hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_
     uint64_t cap = (uint64_t)L.num_cus;  // 148 KiB of LDS: one workgroup per CU
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_tile<WPB, BHG_TILE_NCH, BHG_TILE_PF>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
+    hipLaunchKernelGGL((k_decode_tile<WPB, kTileNch, kTilePf>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
                        expected_crc, out, L.ztab);
     return hipGetLastError();
 }

@@ -238,15 +238,8 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // cycles; dword-aligned stores with a read-back head merge measured 21 % slower.)
 // Checks are the reference decoder's, as in snappy_decode_rt.
 // ---------------------------------------------------------------------------
-#ifndef BHG_SNAPPY_LDS
-#define BHG_SNAPPY_LDS 1
-#endif
-#ifndef BHG_SL_BPW
-#define BHG_SL_BPW 18
-#endif
-#ifndef BHG_SL_SLOT
-#define BHG_SL_SLOT 1088
-#endif
+constexpr uint32_t kSlBpw = 18;     // blocks (lanes) per wave
+constexpr uint32_t kSlSlot = 1088;  // in-place slot bytes per block
 
 // Every LDS access of k_snappy_lds goes through these may_alias types: the slot
 // is written as 16-B chunks and read as bytes, 8-B tags and 16-B chunks, and
@@ -513,9 +506,9 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list) {
-    if (BHG_SNAPPY_LDS && src_len >= 64 && list) {
+    if (src_len >= 64 && list) {
         if (hipError_t e = hipMemsetAsync(list, 0, 4, L.stream)) return e;
-        constexpr uint32_t BPW = BHG_SL_BPW, SLOT = BHG_SL_SLOT;
+        constexpr uint32_t BPW = kSlBpw, SLOT = kSlSlot;
         // resident workgroups per CU (LDS-bound: 8 at 18 x 1,088 B); a grid past that would
         // start its extra workgroups only when the first ones finish
         static const uint32_t per_cu =

@@ -19,33 +19,13 @@
 namespace bhg {
 
 typedef u32x4 u32x4u __attribute__((aligned(1)));
-#ifndef BHG_SE_STAGE16
-#define BHG_SE_STAGE16 1  // measured: C4 30.7 vs 30.0 GiB/s (u16 table: 28.1 at 7 waves, 26.5 at 12)
-#endif
-#ifndef BHG_SE_DCNT
-#define BHG_SE_DCNT 256  // dwords of byte counters for the in-batch duplicate check (4 buckets each)
-#endif
-#ifndef BHG_SE_QUEUE
-#define BHG_SE_QUEUE 1  // values handed to waves by a work queue (0: static round-robin, lab)
-#endif
-#ifndef BHG_SE_HEADS
-#define BHG_SE_HEADS 8  // queue heads per class list
-#endif
-#ifndef BHG_SE_STATIC
-#define BHG_SE_STATIC 75  // % of a class list handed out round-robin before the work queue takes over
-#endif
-#ifndef BHG_SE_WPG
-#define BHG_SE_WPG 3    // waves per workgroup of the large-value launch
-#endif
-#ifndef BHG_SE_UNI
-#define BHG_SE_UNI 1
-#endif
-#ifndef BHG_SE_MINW_SMALL
-#define BHG_SE_MINW_SMALL 4  // waves per SIMD the small-value kernel is compiled for (VGPR budget)
-#endif
-#ifndef BHG_SE_WAVES
-#define BHG_SE_WAVES 7
-#endif
+// Tuning constants, each measured (lab records under profiles/r2*, r3/enc*):
+constexpr uint32_t kSeDcnt = 256;  // dwords of byte counters for the in-batch duplicate check (4 buckets each)
+constexpr uint32_t kSeHeads = 8;   // queue heads per class list
+constexpr uint32_t kSeStatic = 75; // % of a class list handed out round-robin before the work queue takes over
+constexpr int kSeWpg = 3;          // waves per workgroup of the large-value launch
+constexpr int kSeMinwSmall = 4;    // waves per SIMD the small-value kernel is compiled for (VGPR budget)
+constexpr uint32_t kSeWaves = 7;   // resident waves per CU the large-value launch is sized for
 // the hash table holds u16 positions (blocks here are <= 4 KiB): 13 KiB of LDS per wave,
 // 11 waves per CU (a u32 table: 7 waves per CU, 37.7 vs 49.4 GiB/s in round 2)
 typedef uint16_t se_tab_t;
@@ -62,8 +42,8 @@ typedef uint16_t se_tab_t;
 template <int CAP>
 struct SeLayout {
     static constexpr uint32_t kTab = CAP;
-    static constexpr uint32_t kDummy = kTab + 2 * BHG_SE_DCNT;
-    static constexpr uint32_t kWords = (CAP + 16) / 4 + kTab * sizeof(se_tab_t) / 4 + BHG_SE_DCNT + 32;
+    static constexpr uint32_t kDummy = kTab + 2 * kSeDcnt;
+    static constexpr uint32_t kWords = (CAP + 16) / 4 + kTab * sizeof(se_tab_t) / 4 + kSeDcnt + 32;
 };
 
 struct SkipTab {
@@ -236,19 +216,11 @@ __device__ __forceinline__ uint32_t wlane(uint32_t v, uint32_t x, uint32_t i) {
     return (uint32_t)bhg_llvm_writelane((int)x, (int)i, (int)v);
 }
 __device__ __forceinline__ void se_push(OpRing &r, uint32_t lane, uint32_t s, uint32_t e, uint32_t c) {
-#if BHG_SE_UNI
     // s, e, c, r.n are wave-uniform: one v_writelane each
     r.s = wlane(r.s, s, r.n);
     r.e = wlane(r.e, e, r.n);
     r.c = wlane(r.c, c, r.n);
     r.n = uni(r.n + 1);
-#else
-    const bool mine = lane == r.n;
-    r.s = mine ? s : r.s;
-    r.e = mine ? e : r.e;
-    r.c = mine ? c : r.c;
-    r.n++;
-#endif
 }
 
 // lane i <- lane i + 1 (DPP wave_shl:1; lane 63 gets 0)
@@ -277,7 +249,7 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
     // lanes that may share a bucket: per-bucket counts of h mod 1024, one byte per bucket
     // (<= 64 adds per byte); only those lanes are walked
-    const uint32_t slot = (h >> 2) & (BHG_SE_DCNT - 1u), sh8 = 8 * (h & 3);
+    const uint32_t slot = (h >> 2) & (kSeDcnt - 1u), sh8 = 8 * (h & 3);
     const uint32_t one = valid ? 1u << sh8 : 0u;
     atomicAdd(&dcnt[slot], one);  // unconditional: no exec-mask branch
     wsync();
@@ -327,14 +299,10 @@ template <uint32_t DUMMY>
 __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                              uint32_t f0, uint32_t f0n, uint64_t *acc) {
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
-#if BHG_SE_UNI
     len = uni(len);
-#endif
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
-#if BHG_SE_UNI
     shift = uni(shift);
-#endif
     const uint32_t tmask = 16383;
     const uint32_t sLimit = len - SE_MARGIN;
     uint32_t nextEmit = 0, s = 1;
@@ -415,23 +383,17 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
         // prevHash == currHash is resolved by a compare.  So the lookup costs no LDS round
         // trip after the compare; copies ending at s + 64 or later take a serial lookup.
         for (;;) {
-#if BHG_SE_UNI
             // s, cand are wave-uniform; the compiler's divergence analysis cannot see it through
             // the loop's phis and kept them (and everything computed from them) in VGPRs
             s = uni(s);
             cand = uni(cand);
-#endif
             const uint32_t U = ld32a(in32, s + lane);
             const uint32_t V = in[cand + lane];
             const uint32_t hU = se_hash(U, shift) & tmask;
             const uint32_t tU = tab[hU];
             const uint64_t mm = bal((U & 0xffu) != V);
-#if BHG_SE_UNI
             // the first mismatch lane (64: none) as a scalar, so the mins stay SALU
             uint32_t f = min(uni(mm ? (uint32_t)__builtin_ctzll(mm) : 64u), len - s);
-#else
-            uint32_t f = min(mm ? (uint32_t)__builtin_ctzll(mm) : 64u, len - s);
-#endif
             if (f < 4u) {  // the chained candidate does not match: scanning resumes at s + 1
                 Uw = U;
                 hUw = hU;
@@ -442,11 +404,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             while (f == 64u) {
                 r0 += 64;
                 const uint64_t m2 = bal(in[r0 + lane] != in[cand + (r0 - s) + lane]);
-#if BHG_SE_UNI
                 f = min(uni(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u), len - r0);
-#else
-                f = min(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u, len - r0);
-#endif
             }
             const uint32_t e = r0 + f;
             se_push(r, lane, s, e, cand);
@@ -469,16 +427,12 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // the slots coincide both lanes store s)
             const bool same = prevHash == currHash;
             wsync();
-#if BHG_SE_UNI
             // lane 0 stores s - 1 (s when the slots coincide) at prevHash, lane 1 s at currHash,
             // the others s into their scratch slots: two v_writelane per operand
             {
                 const uint32_t ad = wlane(wlane(DUMMY + lane, prevHash, 0), currHash, 1);
                 tab[ad] = (se_tab_t)wlane(s, same ? s : s - 1, 0);
             }
-#else
-            tab[lane == 0 ? prevHash : lane == 1 ? currHash : DUMMY + lane] = (se_tab_t)(lane || same ? s : s - 1);
-#endif
             cand = same ? s - 1 : tc;
             wsync();
             if (r.n == 64) se_flush(o, in, r, lane);
@@ -572,7 +526,7 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (CAP + 16) / 4);
     uint32_t *dcnt = lds + (CAP + 16) / 4 + LY::kTab * sizeof(se_tab_t) / 4;
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t j = lane; j < BHG_SE_DCNT; j += 64) dcnt[j] = 0;
+    for (uint32_t j = lane; j < kSeDcnt; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
     // the small-value launch passes no gtables: its blocks (<= SE_CAP_SMALL) always fit CAP
     uint16_t *gt = gtables != nullptr ? gtables + (size_t)gw * 16384 : nullptr;
@@ -605,18 +559,18 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
         }
         return m;
     };
-    // the first BHG_SE_STATIC % of the list goes round-robin (position cur + nw, no atomic: a
+    // the first kSeStatic % of the list goes round-robin (position cur + nw, no atomic: a
     // queue atomic per value made every wave contend on one address), the rest through the
     // queue (positions qbase + head++), which evens out the end of the launch
-    const uint32_t qbase = BHG_SE_QUEUE ? (uint32_t)((uint64_t)n * BHG_SE_STATIC / 100 / nw * nw) : 0xffffffffu;
+    const uint32_t qbase = (uint32_t)((uint64_t)n * kSeStatic / 100 / nw * nw);
     auto need_q = [&](uint32_t cur) { return cur + nw >= qbase; };
-    // BHG_SE_HEADS queue heads, 128 B apart: wave gw takes from head gw mod H, whose positions are
+    // kSeHeads queue heads, 128 B apart: wave gw takes from head gw mod H, whose positions are
     // qstart + h + H k (the waves of one head are an interleaved H-th of the grid, its positions
     // an interleaved H-th of the queued part: balanced, and H times fewer atomics per address)
-    const uint32_t hq = gw % BHG_SE_HEADS;
+    const uint32_t hq = gw % kSeHeads;
     uint32_t *const myhead = head + 32 * hq;
     auto take = [&](uint32_t cur, uint32_t req) {
-        return need_q(cur) ? max(qbase, nw) + hq + BHG_SE_HEADS * uni(req) : cur + nw;
+        return need_q(cur) ? max(qbase, nw) + hq + kSeHeads * uni(req) : cur + nw;
     };
     uint32_t j = gw;
     Meta mc = meta_of(j, j < n ? list[j] : 0u);
@@ -667,7 +621,6 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
             if (blen < SE_MINNONLIT) {
                 se_emit_literal(o, nullptr, bs, blen, lane);
             } else if (blen <= (uint32_t)CAP) {
-#if BHG_SE_STAGE16
                 // one 16-B load per lane per 1 KiB (one memory round trip), then the 16 zero bytes
                 for (uint32_t t = 16 * lane; t < blen; t += 1024) {
                     u32x4 v;
@@ -681,9 +634,6 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
                     *reinterpret_cast<u32x4 *>(in + t) = v;
                 }
                 wsync();
-#else
-                for (uint32_t t = lane; t < blen; t += 64) in[t] = bs[t];
-#endif
                 for (uint32_t t = blen + lane; t < blen + 16; t += 64) in[t] = 0;
                 uint32_t ts = 256;
                 while (ts < 16384 && ts < blen) ts *= 2;
@@ -786,21 +736,18 @@ __global__ __launch_bounds__(64 * kClassWaves) void k_enc_class(const uint64_t *
 // what is resident would start its extra workgroups only when the first ones finish
 template <int CAP, int WPG, int MINW>
 static uint32_t enc_grid(const Launch &L, uint32_t n) {
-    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP, WPG, MINW>, 64 * WPG, BHG_SE_WAVES / WPG);
+    static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_enc<CAP, WPG, MINW>, 64 * WPG, kSeWaves / WPG);
     uint32_t pc = per_cu;
-#ifdef BHG_SE_MAXW  // lab: fewer resident waves per CU, to see how the encoder scales with occupancy
-    if (pc * WPG > BHG_SE_MAXW) pc = BHG_SE_MAXW / WPG;
-#endif
     uint32_t g = (uint32_t)L.num_cus * pc;
     if ((uint64_t)g * WPG > n) g = (n + WPG - 1) / WPG;
     return g ? g : 1;
 }
 
 // waves of the large-value launch (one global hash table each for blocks > SE_CAP)
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n) * BHG_SE_WPG; }
+uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, kSeWpg, 3>(L, n) * kSeWpg; }
 
-// class lists (2n), class counts (4 words), then 2 x BHG_SE_HEADS queue heads of 32 words each
-constexpr uint32_t kQueueWords = 4 + 2 * BHG_SE_HEADS * 32;
+// class lists (2n), class counts (4 words), then 2 x kSeHeads queue heads of 32 words each
+constexpr uint32_t kQueueWords = 4 + 2 * kSeHeads * 32;
 size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + kQueueWords) * 4; }
 
 hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
@@ -816,11 +763,11 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
     // <= SE_CAP_SMALL = its LDS capacity), so it gets no global hash tables: gtables is sized for
     // the large-value grid only (snappy_enc_grid)
     static_assert(SE_CAP_SMALL <= SE_CAP, "small-value class must fit the LDS block");
-    hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>), dim3(enc_grid<SE_CAP_SMALL, 1, BHG_SE_MINW_SMALL>(L, n)), dim3(64), 0, L.stream, vals,
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, kSeMinwSmall>), dim3(enc_grid<SE_CAP_SMALL, 1, kSeMinwSmall>(L, n)), dim3(64), 0, L.stream, vals,
                        val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen, nullptr);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((k_snappy_enc<SE_CAP, BHG_SE_WPG, 3>), dim3(enc_grid<SE_CAP, BHG_SE_WPG, 3>(L, n)), dim3(64 * BHG_SE_WPG), 0,
-                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * BHG_SE_HEADS, scratch, scap, soff, clen,
+    hipLaunchKernelGGL((k_snappy_enc<SE_CAP, kSeWpg, 3>), dim3(enc_grid<SE_CAP, kSeWpg, 3>(L, n)), dim3(64 * kSeWpg), 0,
+                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * kSeHeads, scratch, scap, soff, clen,
                        gtables);
     return hipGetLastError();
 }

@@ -73,21 +73,20 @@ def test_no_selectable_kernel_variants():
 
 def _src_default(fname, knob):
     src = open(os.path.join(os.path.dirname(B.LIB_PATH), "..", "csrc", fname)).read()
-    m = re.search(r"#define %s (\d+)" % knob, src)
+    m = re.search(r"constexpr (?:int|uint32_t) %s = (\d+);" % knob, src)
     assert m, (fname, knob)
     return int(m.group(1))
 
 
 def test_shipped_library_has_default_knobs():
-    """The .so was built with the sources' default compile knobs: each templated kernel exists
-    in exactly the instantiation its file's #define defaults select (a lab build with -D knobs
-    would ship a different one)."""
+    """The .so holds exactly the kernel instantiations the sources' tuning constants select
+    (no compile-time knobs remain; a stale or lab-built object would ship a different one)."""
     B.build()
     blob = open(B.LIB_PATH, "rb").read()
-    pf = _src_default("bhg_decode_tile.hip", "BHG_TILE_PF")
-    nch = _src_default("bhg_decode_tile.hip", "BHG_TILE_NCH")
-    bpw = _src_default("bhg_snappy_dec.hip", "BHG_SL_BPW")
-    slot = _src_default("bhg_snappy_dec.hip", "BHG_SL_SLOT")
+    pf = _src_default("bhg_decode_tile.hip", "kTilePf")
+    nch = _src_default("bhg_decode_tile.hip", "kTileNch")
+    bpw = _src_default("bhg_snappy_dec.hip", "kSlBpw")
+    slot = _src_default("bhg_snappy_dec.hip", "kSlSlot")
     want = {
         rb"_ZN3bhg13k_decode_tileI": b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf),
         rb"_ZN3bhg12k_snappy_ldsI": b"_ZN3bhg12k_snappy_ldsILi%dELi%dEE" % (bpw, slot),

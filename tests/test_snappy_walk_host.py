@@ -20,7 +20,7 @@ from oracle import oracle as O
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "bitalosdb_amd", "csrc", "bhg_snappy_dec.hip")
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
-SLOT = 1088  # BHG_SL_SLOT
+SLOT = 1088  # kSlSlot (bhg_snappy_dec.hip)
 
 
 @pytest.fixture(scope="module")
