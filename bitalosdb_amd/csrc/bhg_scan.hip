@@ -1,8 +1,9 @@
 // bhg_scan.hip -- exclusive prefix sum over u64 (decoded-size -> output
 // offsets for snappy values, record lengths -> record positions for encode).
-// Reduce-then-scan: per-workgroup chunk sums, a recursive scan of the sums,
-// then a chunk-local scan plus base.  Each workgroup covers 2048 elements
-// (256 threads x 8), so 1M sizes need 489 workgroups and one recursion level.
+// Reduce-then-scan: per-workgroup chunk sums, then a chunk-local scan plus base, the base
+// summed by each workgroup from the chunk sums before it (up to 4,096 chunks = 8M elements;
+// larger inputs scan the sums recursively).  Each workgroup covers 2048 elements (256
+// threads x 8), so 1M sizes need 489 workgroups.
 #include "bhg_internal.h"
 
 namespace bhg {
@@ -76,6 +77,36 @@ __global__ __launch_bounds__(SCAN_T) void k_chunk_scan(const uint64_t *in, uint6
     if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_T - 1) out[n] = run;
 }
 
+// chunk-local exclusive scan whose base is summed here from the chunk sums before it (nb <=
+// kDirectChunks: at most 16 per thread, read from L2), the last chunk writing the total: two
+// launches per scan instead of four (sums, recursive scan of the sums, chunk scan, total copy)
+constexpr uint64_t kDirectChunks = SCAN_T * 16;
+__global__ __launch_bounds__(SCAN_T) void k_chunk_scan_direct(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                              const uint64_t *__restrict__ sums) {
+    uint64_t pre = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += SCAN_T) pre += sums[k];
+    uint64_t base;
+    block_excl_scan(pre, &base);
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_CHUNK;
+    uint64_t v[SCAN_PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        uint64_t idx = b0 + (uint64_t)threadIdx.x * SCAN_PER + k;
+        v[k] = idx < n ? in[idx] : 0;
+        s += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(s, &tot) + base;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        uint64_t idx = b0 + (uint64_t)threadIdx.x * SCAN_PER + k;
+        if (idx < n) out[idx] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_T - 1) out[n] = run;
+}
+
 size_t scan_scratch_bytes(uint64_t n) {
     size_t bytes = 0;
     while (n > SCAN_CHUNK) {
@@ -98,6 +129,11 @@ hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64
     uint64_t *sums = reinterpret_cast<uint64_t *>(scratch);
     uint8_t *rest = reinterpret_cast<uint8_t *>(scratch) + (nb + 1) * sizeof(uint64_t);
     hipLaunchKernelGGL(k_chunk_sums, dim3((uint32_t)nb), dim3(SCAN_T), 0, L.stream, in, n, sums);
+    if (nb <= kDirectChunks) {
+        hipLaunchKernelGGL(k_chunk_scan_direct, dim3((uint32_t)nb), dim3(SCAN_T), 0, L.stream, in, out, n,
+                           (const uint64_t *)sums);
+        return hipGetLastError();
+    }
     hipError_t e = launch_exclusive_scan_u64(L, sums, sums, nb, rest);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_chunk_scan, dim3((uint32_t)nb), dim3(SCAN_T), 0, L.stream, in, out, n, (const uint64_t *)sums, 0);

@@ -323,3 +323,27 @@ def test_tail_one_key_under_two_khash(codec):
         exp, w = _oracle_ikey_table(keys, trs, vals, khash)
         assert int(stats[0, 1]) == len(w.conflict_keys)
         assert got == exp, spec[:5]
+
+
+def test_tail_conflict_keys_prefix_edge_cases(codec):
+    """k_conf_rank / k_tail_dedupe compare keys by their big-endian 8-byte prefix first and
+    fall back to the bytes only on equal prefixes: keys that are prefixes of each other, keys
+    with zero bytes where the prefix pads with zeros, keys shorter than 8 B, the empty key, and
+    keys equal in the first 8 bytes -- one conflict group, plus a second group holding some of
+    the same keys (dedupe across two khash values)."""
+    rng = random.Random(43)
+    edge = [b"", b"\x00", b"\x00\x00", b"a", b"a\x00", b"a\x00\x00", b"a\x00b", b"ab", b"abcdefgh",
+            b"abcdefgh\x00", b"abcdefgh\x00\x00", b"abcdefghi", b"abcdefgh\xff", b"abcdefg", b"\xff" * 9]
+    A, B = 0x5A5A0001, 0x5A5A0002
+    spec = [(k, A) for k in edge]
+    spec += [(b"a\x00", B), (b"abcdefgh", B), (b"zz", B), (b"a\x00", A), (b"", B)]
+    spec += [(b"fill_%d" % i, O.fnv32(b"fill_%d" % i)) for i in range(20)]
+    rng.shuffle(spec)
+    keys = [k for k, _ in spec]
+    khash = [h for _, h in spec]
+    trs = [((i + 1) << 8) | 1 for i in range(len(spec))]
+    vals = [rb(rng, rng.choice([1, 9, 70])) for _ in spec]
+    got, stats = _ikey_table(codec, keys, trs, vals, khash)
+    exp, w = _oracle_ikey_table(keys, trs, vals, khash)
+    assert int(stats[0, 1]) == len(w.conflict_keys)
+    assert got == exp
