@@ -348,12 +348,12 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
             n = (b14 & lmask) + 1u;
             adv = 1u + nb;
         }
-        const uint32_t rem = se - s;  // >= 1
-        // checks of decode_other.go (n == 0 only for a 4-byte literal length of 2^32 - 1: too long)
-        const uint32_t bad_lit = (uint32_t)(n > rem - adv), bad_cp = (uint32_t)(off == 0u) | (uint32_t)(off > d);
-        const bool bad = ((uint32_t)(adv > rem) | (uint32_t)(n > dlen - d) | (uint32_t)(n == 0u) |
-                          (mlit & bad_lit) | (~mlit & bad_cp)) != 0u;
+        // checks of decode_other.go, three compares: n - 1 >= dlen - d is n == 0 (a 4-byte literal
+        // length of 2^32 - 1) or an element past dlen; sn > se is a tag (or a literal's bytes)
+        // past the stream -- sn cannot wrap once n <= dlen - d <= 1 KiB; off - 1 >= d is a copy
+        // offset of 0 or past the bytes written
         const uint32_t sn = s + adv + (mlit & n);
+        const bool bad = ((uint32_t)(n - 1u >= dlen - d) | (uint32_t)(sn > se) | (~mlit & (uint32_t)(off - 1u >= d))) != 0u;
         const bool spill = op + d + n + 16u > sn;  // 16-B ops write below op + d + n + 16; the next tag is at sn
         if (bad | spill) {
             res = bad ? 1u : 2u;
