@@ -98,7 +98,8 @@ typedef struct bhg_handle {
  *                     computed whenever the handle lies inside src
  *   status          : BHG_ST_*
  * For RECORD_NIL / ILLEGAL_LENGTH / INCOMPLETE every field except crc and
- * status is 0.  For SNAPPY_* the key fields are filled, val_off/val_len 0. */
+ * status is 0.  For SNAPPY_* the key fields are filled, val_off/val_len 0, and the block's
+ * slot in out_vals (out_val_off[i] .. [i+1]) holds unspecified bytes. */
 typedef struct bhg_desc {
     uint32_t key_off, key_len;
     uint32_t val_off, val_len;

@@ -696,3 +696,53 @@ def test_host_pipelined_then_unsorted(pin, monkeypatch):
     assert_desc_equal(got, exp)
     assert (got["status"] == O.CRC_MISMATCH).sum() > 0
     c.close()
+
+
+@pytest.mark.parametrize("seed", [101, 202])
+def test_fuzz_corrupt_records(codec, seed):
+    """Randomised corruption of valid records, both codecs, every descriptor field and
+    decoded byte against the restatement: flipped bytes in the 12-B header (key / value
+    sizes, fileNum), in the key, trailer and value or snappy stream; handles cut short,
+    stretched past the record or past src, zero-length; expected CRCs wrong for some."""
+    rng = random.Random(seed)
+    n = 4000
+    for cdc in (0, 1):
+        specs = []
+        for i in range(n):
+            kl = rng.choice([0, 1, 7, 8, 20, 32, 40])
+            vl = rng.choice([1, 5, 60, 200, 1024, 1500])
+            v = bytes((b"snappy-" * 300)[:vl]) if rng.random() < 0.5 else rand_bytes(rng, vl)
+            specs.append((rand_bytes(rng, kl), v, 1 + i % 5))
+        src, h = make_records(rng, specs, gap_max=3, codec=cdc)
+        buf = bytearray(src)
+        h = h.copy()
+        crc = np.array([O.crc_masked(bytes(buf[int(o):int(o) + int(ln)])) for o, ln in zip(h["offset"], h["length"])],
+                       dtype=np.uint32)
+        for i in range(n):
+            o, ln = int(h["offset"][i]), int(h["length"][i])
+            r = rng.random()
+            if r < 0.10:      # a header byte (key size, value size or fileNum)
+                buf[o + rng.randrange(12)] ^= 1 << rng.randrange(8)
+            elif r < 0.25:    # a byte of the key, trailer or value / snappy stream
+                if ln > 12:
+                    buf[o + 12 + rng.randrange(ln - 12)] ^= 1 << rng.randrange(8)
+            elif r < 0.30:    # handle cut short
+                h["length"][i] = rng.randrange(ln)
+            elif r < 0.33:    # handle stretched into the next record
+                h["length"][i] = ln + rng.randrange(1, 64)
+            elif r < 0.35:    # handle past src
+                h["offset"][i] = len(buf) - rng.randrange(1, 32)
+            elif r < 0.40:    # a wrong expected CRC
+                crc[i] ^= 1 << rng.randrange(32)
+        got, gv, go = codec.decode(bytes(buf), h, compressor=cdc, expected_crc=crc)
+        exp, ev, eo = O.decode_batch(bytes(buf), h, codec=cdc, expected_crc=crc)
+        assert_desc_equal(got, exp)
+        if cdc == 1:
+            # decoded values of the blocks Decode returns (OK, or OK but CRC-mismatched); a
+            # corrupt block's slot holds no value (the reference returns snappy.ErrCorrupt)
+            assert np.array_equal(go, eo)
+            for i in np.nonzero((exp["status"] == 0) | (exp["status"] == 6))[0]:
+                a, b = int(eo[i]), int(eo[i + 1])
+                assert gv[a:b].tobytes() == ev[a:b].tobytes(), (i, int(exp["status"][i]))
+        st = np.bincount(exp["status"], minlength=16)
+        assert st[0] > n // 2 and (st[1:] > 0).sum() >= 3, st   # most OK, several failure kinds hit
