@@ -188,7 +188,7 @@ int bhg_host_unregister(bhg_ctx *ctx, void *p);
  * such range).  Handles past src_len give 0. */
 int bhg_crc32c_masked_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                             uint32_t n, uint32_t *out_crc, void *stream);
-/* Same result as bhg_crc32c_masked_batch, one workgroup per range: for a few
+/* Same result as bhg_crc32c_masked_batch, each range spread over up to 64 workgroups: for
  * LONG ranges, e.g. verifying each table's indexhash_checksum
  * (bithash/writer.go:476-478 writes crc.New(indexhash_data).Value() as decimal;
  * bithash/reader.go:162-190 (readIndexHash) reads only indexhash_data, never the checksum -- SURVEY
