@@ -30,7 +30,8 @@
 #include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
 #include "../../../bitalosdb_amd/csrc/bhg_device.h"
 #include "../../../include/bithashgpu.h"
-#include "decode_dma_kernel.hip"  // the product-shaped DMA kernel (lab), timed beside the product tile kernel
+#include "decode_dma_kernel.hip"
+#include "tile_nb3.hip"  // the product-shaped DMA kernel (lab), timed beside the product tile kernel
 #include "../../../bitalosdb_amd/csrc/bhg_decode_tile.hip"
 
 #define CK(x)                                                                                  \
@@ -439,6 +440,13 @@ static void launch_product(const uint8_t *src, uint64_t len, const bhg_handle *h
 }
 
 static uint32_t *g_ztab = nullptr;
+static void launch_nb3(const uint8_t *src, uint64_t len, const bhg_handle *h, uint32_t n, const uint32_t *ec,
+                       bhg_desc *out, const uint32_t *, int cus, hipStream_t s) {
+    const uint64_t tiles = (n + 63) / 64;
+    uint64_t need = (tiles + 7) / 8;
+    uint32_t grid = (uint32_t)(need < (uint64_t)cus ? need : cus);
+    hipLaunchKernelGGL((bhg::nb3::k_decode_tile_nb3<8, 2, 0>), dim3(grid), dim3(512), 0, s, src, len, h, n, ec, out, g_ztab);
+}
 template <int PF, int WPB = 8, int NCH = 2>
 static void launch_tile(const uint8_t *src, uint64_t len, const bhg_handle *h, uint32_t n, const uint32_t *ec,
                         bhg_desc *out, const uint32_t *, int cus, hipStream_t s) {
@@ -505,9 +513,8 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&g_ztab, zt.size() * 4));
         CK(hipMemcpy(g_ztab, zt.data(), zt.size() * 4, hipMemcpyHostToDevice));
     }
-    const V vs[] = {{"tile_pf2", launch_tile<2>}, {"tile_pf2_w12", launch_tile<2, 12>}, {"tile_pf0_w12", launch_tile<0, 12>},
-                    {"tile_pf2_w12_n1", launch_tile<2, 12, 1>}, {"tile_pf2_n1", launch_tile<2, 8, 1>},
-                    {"tile_pf2_b", launch_tile<2>}, {"tile_pf2_w12_b", launch_tile<2, 12>}, {"tile_pf2_w12_n1_b", launch_tile<2, 12, 1>}};
+    const V vs[] = {{"tile_pf2", launch_tile<2>}, {"tile_nb3", launch_nb3}, {"tile_pf0", launch_tile<0>},
+                    {"tile_pf2_b", launch_tile<2>}, {"tile_nb3_b", launch_nb3}, {"tile_pf0_b", launch_tile<0>}};
     auto prod = [&]() { if (bhg_decode_batch(ctx, src, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
     for (int it = 0; it < 200; it++) prod();  // clocks
     CK(hipStreamSynchronize(s));
