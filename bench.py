@@ -771,6 +771,45 @@ def c3_measure(a, world, rank, local, dev, codec, gen, extras):
                                "one_thread: the first %d blocks on 1 thread (%s)" % (reps, n, thr, n1, cpu_info())}
         out["parity_vs_restatement"] = "bit-exact" if par else "MISMATCH"
         out["valid"] = bool(out["valid"] and par)
+    if extras and rank == 0 and world == 1 and not a.no_e2e:
+        # end-to-end: host table bytes -> H2D -> header/CRC pass + scan + snappy -> D2H descriptors, value
+        # offsets and the decoded values (bhg_decode_batch_host; snappy stages the whole src in HBM).
+        # Caller-owned output buffers are reused; pageable first, then page-locked (bhg_host_register).
+        host_src = src.cpu().numpy()
+        ecrc_h = exp_crc.cpu().numpy().view(np.uint32).copy()
+        host_desc = np.empty(n, dtype=DESC_DT)
+        host_vals = np.empty(n * 1024 + 64, dtype=np.uint8)
+        e2e = {}
+        for mode in ("pageable", "pinned"):
+            bufs = (host_src, host_desc, host_vals, h, ecrc_h)
+            if mode == "pinned":
+                for b in bufs:
+                    codec.host_register(b)
+            run = lambda: codec.decode_host(host_src, h, compressor=1, expected_crc=ecrc_h,
+                                            out_desc=host_desc, out_vals=host_vals)
+            run()
+            reps, t = 3, time.perf_counter()
+            for _ in range(reps):
+                got_d, got_v, _ = run()
+            e2e_s = (time.perf_counter() - t) / reps
+            e2e[mode] = round(disk / e2e_s / 2 ** 30, 3)
+            if mode == "pinned":
+                for b in bufs[::-1]:
+                    codec.host_unregister(b)
+        d_vals = vals.cpu().numpy()
+        nv = got_v.size
+        host_ok = bool(all(np.array_equal(got_d[f], d[f]) for f in d.dtype.names)
+                       and np.array_equal(got_v, d_vals[:nv]))
+        out["e2e_host"] = {"value": e2e["pinned"], "unit": "GiB/s on disk", "pageable": e2e["pageable"],
+                           "decoded_GiBps_pinned": round(e2e["pinned"] * n * 1024 / disk, 3),
+                           "matches_device_path": host_ok,
+                           "note": "host src (%.2f GB) + handles + expected CRCs -> descriptors, value offsets and "
+                                   "%.2f GB of decoded values in host memory: 64 MiB src chunks, chunk k + 1's H2D "
+                                   "under chunk k's values going back (a copy kernel into the mapped out_vals when "
+                                   "it is page-locked, else D2H copies), caller-owned output buffers reused.  value: "
+                                   "all host buffers page-locked (bhg_host_register); pageable also given"
+                                   % (host_src.size / 1e9, n * 1024 / 1e9)}
+        out["valid"] = bool(out["valid"] and host_ok)
     return out
 
 

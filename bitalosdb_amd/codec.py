@@ -168,12 +168,14 @@ class BithashCodec:
         return res.desc_np(), None, None
 
     def decode_host(self, src, handles, compressor=NoCompressor, expected_crc=None, out_vals_cap=None,
-                    out_desc=None):
+                    out_desc=None, out_vals=None):
         """End-to-end path: host buffers in and out (bhg_decode_batch_host).
         Snappy with out_vals_cap None runs the sizing pass first (out_vals NULL)
         and allocates exactly out_val_off[n] bytes.  out_desc: an optional
         caller-owned DESC_DT array of n entries (e.g. host_register'ed once and
-        reused: the NoCompressor path then writes it in place)."""
+        reused: the NoCompressor path then writes it in place).  out_vals: an
+        optional caller-owned contiguous uint8 array for the snappy values (its
+        size is the capacity when out_vals_cap is None; no sizing pass then)."""
         src = np.ascontiguousarray(np.frombuffer(src, np.uint8) if isinstance(src, (bytes, bytearray)) else src,
                                    dtype=np.uint8)
         h = np.ascontiguousarray(handles, dtype=HANDLE_DT)
@@ -189,13 +191,17 @@ class BithashCodec:
         cap = 0
         vals = None
         if compressor == SnappyCompressor:
+            if out_vals is not None:
+                if out_vals.dtype != np.uint8 or out_vals.ndim != 1 or not out_vals.flags["C_CONTIGUOUS"]:
+                    raise ValueError("out_vals must be a contiguous 1-D uint8 array")
+                out_vals_cap = out_vals.size if out_vals_cap is None else min(out_vals_cap, out_vals.size)
             if out_vals_cap is None:
                 rc = self.L.bhg_decode_batch_host(self.ctx, _ptr(src), src.size, _ptr(h), n, compressor, _ptr(exp),
                                                   _ptr(desc), None, 0, _ptr(off))
                 B.check(self.ctx, rc, "bhg_decode_batch_host(sizing)")
                 out_vals_cap = int(off[-1])
             cap = out_vals_cap
-            vals = np.zeros(max(cap, 1), dtype=np.uint8)
+            vals = out_vals if out_vals is not None else np.zeros(max(cap, 1), dtype=np.uint8)
         rc = self.L.bhg_decode_batch_host(self.ctx, _ptr(src), src.size, _ptr(h), n, compressor, _ptr(exp),
                                           _ptr(desc), _ptr(vals), cap, _ptr(off))
         B.check(self.ctx, rc, "bhg_decode_batch_host")

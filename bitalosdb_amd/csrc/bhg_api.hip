@@ -37,6 +37,13 @@ struct bhg_ctx {
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
     void *pbuf[kPipe] = {nullptr, nullptr, nullptr};
     size_t pbuf_cap[kPipe] = {0, 0, 0};
+    // ... the snappy pipeline's per-slot decoded values, chunk totals (page-locked) and their events
+    void *pvals[kPipe] = {nullptr, nullptr, nullptr};
+    size_t pvals_cap[kPipe] = {0, 0, 0};
+    uint64_t *ptot = nullptr;
+    hipEvent_t pev[kPipe] = {nullptr, nullptr, nullptr};   // chunk total in ptot
+    hipEvent_t pevb[kPipe] = {nullptr, nullptr, nullptr};  // chunk values decoded
+    hipEvent_t pevd[kPipe] = {nullptr, nullptr, nullptr};  // chunk copied back (slot free)
 };
 
 namespace {
@@ -195,7 +202,12 @@ void bhg_destroy(bhg_ctx *c) {
     for (int k = 0; k < bhg_ctx::kPipe; k++) {
         if (c->pstream[k]) { (void)hipStreamSynchronize(c->pstream[k]); (void)hipStreamDestroy(c->pstream[k]); }
         if (c->pbuf[k]) (void)hipFree(c->pbuf[k]);
+        if (c->pvals[k]) (void)hipFree(c->pvals[k]);
+        if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
+        if (c->pevb[k]) (void)hipEventDestroy(c->pevb[k]);
+        if (c->pevd[k]) (void)hipEventDestroy(c->pevd[k]);
     }
+    if (c->ptot) (void)hipHostFree(c->ptot);
     if (c->h_src) (void)hipFree(c->h_src);
     if (c->h_aux) (void)hipFree(c->h_aux);
     if (c->h_vals) (void)hipFree(c->h_vals);
@@ -310,6 +322,44 @@ namespace {
 // kernels and copies of the others; slot reuse is ordered by its stream.
 constexpr uint64_t kChunkBytesDefault = 64ull << 20;
 
+// The next chunk [a, return) of the pipelined host paths: grown while the in-bounds records' byte
+// span [*lo, *hi) of src stays within chunk_bytes (a record larger than that makes a chunk of its
+// own) and at most max_cn handles.  A handle whose offset is below its predecessor's (*prev_off,
+// carried across calls) ends the chunk before it and sets *unsorted.
+uint32_t next_chunk(const bhg_handle *handles, uint32_t a, uint32_t n, uint64_t src_len, uint64_t chunk_bytes,
+                    uint32_t max_cn, uint64_t *prev_off, uint64_t *lo_out, uint64_t *hi_out, bool *unsorted) {
+    uint64_t lo = UINT64_MAX, hi = 0;
+    uint32_t b = a;
+    while (b < n && b - a < max_cn) {
+        const bhg_handle &h = handles[b];
+        if (h.offset < *prev_off) {
+            *unsorted = true;
+            break;
+        }
+        *prev_off = h.offset;
+        const bool inb = h.length != 0 && h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
+        if (inb) {
+            const uint64_t nlo = h.offset < lo ? h.offset : lo;
+            const uint64_t nhi = h.offset + h.length > hi ? h.offset + h.length : hi;
+            if (b > a && nhi - nlo > chunk_bytes) break;
+            if (nhi - nlo > chunk_bytes) { lo = nlo; hi = nhi; b++; break; }  // one oversized record
+            lo = nlo;
+            hi = nhi;
+        }
+        b++;
+    }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    *lo_out = lo;
+    *hi_out = hi;
+    return b;
+}
+
+uint64_t host_chunk_bytes() {
+    uint64_t v = kChunkBytesDefault;
+    if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) v = strtoull(e, nullptr, 10);  // tests
+    return v < 4096 ? 4096 : v;
+}
+
 // Handles out of offset order end the pipeline where they start: the chunk walk below checks the order
 // as it goes (no separate host pass over the batch), the chunks already issued complete, and the
 // function returns -100 with *done = the handles decoded; the caller decodes the rest another way.
@@ -317,9 +367,7 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
                           const uint32_t *expected_crc, bhg_desc *out_desc, uint32_t *done) {
     *done = 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    uint64_t kChunkBytes = kChunkBytesDefault;
-    if (const char *e = getenv("BHG_HOST_CHUNK_BYTES")) kChunkBytes = strtoull(e, nullptr, 10);  // tests
-    if (kChunkBytes < 4096) kChunkBytes = 4096;
+    const uint64_t kChunkBytes = host_chunk_bytes();
     const uint32_t max_chunk_n = 1u << 17;
     // kHead bytes of headroom before each chunk's src bytes: the decode kernels may load (and mask) a
     // window that starts up to 131 B before a record, which must be mapped memory
@@ -336,29 +384,9 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     uint64_t prev_off = 0;
     bool unsorted = false;
     while (a < n) {
-        // grow the chunk while its byte span stays within kChunkBytes
-        uint64_t lo = UINT64_MAX, hi = 0;
-        uint32_t b = a;
-        while (b < n && b - a < max_chunk_n) {
-            const bhg_handle &h = handles[b];
-            if (h.offset < prev_off) {
-                unsorted = true;
-                break;
-            }
-            prev_off = h.offset;
-            const bool inb = h.length != 0 && h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
-            if (inb) {
-                const uint64_t nlo = h.offset < lo ? h.offset : lo;
-                const uint64_t nhi = h.offset + h.length > hi ? h.offset + h.length : hi;
-                if (b > a && nhi - nlo > kChunkBytes) break;
-                if (nhi - nlo > kChunkBytes) { lo = nlo; hi = nhi; b++; break; }  // one oversized record
-                lo = nlo;
-                hi = nhi;
-            }
-            b++;
-        }
+        uint64_t lo, hi;
+        const uint32_t b = next_chunk(handles, a, n, src_len, kChunkBytes, max_chunk_n, &prev_off, &lo, &hi, &unsorted);
         const uint32_t cn = b - a;
-        if (lo == UINT64_MAX) lo = hi = 0;
         const uint64_t span = hi - lo;
         if (span > kChunkBytes || cn == 0) {
             // a single record larger than the ring slot, or handles out of order from a on: the caller
@@ -394,6 +422,166 @@ int decode_host_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     }
     for (int k = 0; k < bhg_ctx::kPipe; k++) HIP_TRY(c, hipStreamSynchronize(c->pstream[k]));
     *done = n;
+    return BHG_OK;
+}
+
+const void *mapped_device_ptr(const void *p);
+
+// Pipelined end-to-end SnappyCompressor decode for handles sorted by offset, every in-bounds
+// record within one chunk (else -100 before anything is issued: the caller decodes the whole
+// batch at once).  Two streams: the context stream carries the H2D copies and the kernels, a
+// second one the D2H copies, so chunk k + 1's H2D runs under chunk k's D2H (PCIe carries both
+// directions at once).  Per chunk k, in slot k % kPipe:
+//   A (context stream): H2D of its src byte range [lo, hi), handles and expected CRCs; the
+//     handles rebased onto the staged range (the kernels see a source of hi - lo bytes: they
+//     may load from its first bytes on behalf of any lane, so the source they are given must
+//     be mapped from its start); the header/CRC pass; the chunk-local size scan; D2H of the
+//     chunk total into page-locked ptot[slot] (event pev).
+//   B (context stream, once the host has that total): the offsets rebased onto the batch and
+//     the value decode into the slot's value buffer (event pevb).  The decode gets out_vals =
+//     slot buffer - batch base and a cap of min(out_vals_cap, base + chunk total): the same
+//     SNAPPY_TOO_LARGE verdicts as one batch-wide launch.
+//   D (copy stream, after pevb): values, offsets and descriptors back to the host (event pevd,
+//     which A of the chunk that next takes the slot waits for).  Values into a page-locked,
+//     mapped out_vals go by a copy kernel (k_copy_out: the link rate; a D2H copy may get a DMA
+//     engine that runs at half of it), else by a D2H copy; the slot buffer then holds them at
+//     the host address's offset mod 16.
+// The host issues B(k), A(k + 1), D(k) in that order, so an H2D is always queued before the
+// D2H it should overlap (a D2H call may return only when its copy is done).  Rebasing keeps
+// every status: in-bounds records lie in [lo, hi); the others stay past the end (the offsets
+// of those below lo wrap).
+int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
+                                 uint32_t n, const uint32_t *expected_crc, bhg_desc *out_desc, uint8_t *out_vals,
+                                 uint64_t out_vals_cap, uint64_t *out_val_off) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const uint64_t kChunkBytes = host_chunk_bytes();
+    {
+        uint64_t prev = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const bhg_handle &h = handles[i];
+            if (h.offset < prev) return -100;
+            prev = h.offset;
+            const bool inb = h.length != 0 && h.offset <= src_len && (uint64_t)h.length <= src_len - h.offset;
+            if (inb && h.length > kChunkBytes) return -100;
+        }
+    }
+    const uint32_t max_chunk_n = 1u << 17;
+    const size_t b_src = al(kChunkBytes + 64), b_h = al((size_t)max_chunk_n * sizeof(bhg_handle));
+    const size_t b_d = al((size_t)max_chunk_n * sizeof(bhg_desc)), b_e = al((size_t)max_chunk_n * 4);
+    const size_t b_o = al(((size_t)max_chunk_n + 1) * 8), b_s = al(bhg::scan_scratch_bytes(max_chunk_n));
+    const size_t b_l = al(bhg::snappy_list_bytes(max_chunk_n));
+    const size_t need = b_src + b_h + b_d + b_e + b_o + b_s + b_l;
+    if (!c->pstream[0]) HIP_TRY(c, hipStreamCreateWithFlags(&c->pstream[0], hipStreamNonBlocking));
+    for (int k = 0; k < bhg_ctx::kPipe; k++) {
+        if (!c->pev[k]) HIP_TRY(c, hipEventCreateWithFlags(&c->pev[k], hipEventDisableTiming));
+        if (!c->pevb[k]) HIP_TRY(c, hipEventCreateWithFlags(&c->pevb[k], hipEventDisableTiming));
+        if (!c->pevd[k]) HIP_TRY(c, hipEventCreateWithFlags(&c->pevd[k], hipEventDisableTiming));
+        if (int r = ensure_buf(c, &c->pbuf[k], &c->pbuf_cap[k], need)) return r;
+    }
+    if (!c->ptot) HIP_TRY(c, hipHostMalloc(reinterpret_cast<void **>(&c->ptot), bhg_ctx::kPipe * sizeof(uint64_t),
+                                           hipHostMallocDefault));
+    struct Slot {
+        uint8_t *src;
+        bhg_handle *h;
+        bhg_desc *d;
+        uint32_t *e;
+        uint64_t *off;
+        void *scan;
+        uint32_t *list;
+    };
+    auto slot_of = [&](int k) {
+        uint8_t *p = reinterpret_cast<uint8_t *>(c->pbuf[k]);
+        Slot S;
+        S.src = p; p += b_src;
+        S.h = reinterpret_cast<bhg_handle *>(p); p += b_h;
+        S.d = reinterpret_cast<bhg_desc *>(p); p += b_d;
+        S.e = expected_crc ? reinterpret_cast<uint32_t *>(p) : nullptr; p += b_e;
+        S.off = reinterpret_cast<uint64_t *>(p); p += b_o;
+        S.scan = p; p += b_s;
+        S.list = reinterpret_cast<uint32_t *>(p);
+        return S;
+    };
+    struct Chunk {
+        uint32_t a, cn;
+        int slot;
+        uint64_t lo, hi, vb, fit;  // vb, fit, mis: set by stage B (batch value base, bytes copied back,
+        uint32_t mis;              // the values' offset in the slot buffer)
+    };
+    bhg::Launch L = launch_of(c, nullptr);  // the context stream
+    hipStream_t sc = c->stream, sd = c->pstream[0];
+    bhg::Launch Ld = L;
+    Ld.stream = sd;
+    uint8_t *mvals = const_cast<uint8_t *>(static_cast<const uint8_t *>(mapped_device_ptr(out_vals)));
+    bool dpend[bhg_ctx::kPipe] = {false, false, false};  // the slot's last D2H has an event to wait for
+    uint64_t vbase = 0;                                   // the batch offset of the next chunk's first value
+    uint64_t prev_off = 0;
+    bool unsorted = false;  // cannot happen: checked above
+    auto stage_a = [&](Chunk &ch) -> int {
+        const Slot S = slot_of(ch.slot);
+        if (dpend[ch.slot]) HIP_TRY(c, hipStreamWaitEvent(sc, c->pevd[ch.slot], 0));
+        if (ch.hi > ch.lo) HIP_TRY(c, hipMemcpyAsync(S.src, src + ch.lo, ch.hi - ch.lo, hipMemcpyHostToDevice, sc));
+        HIP_TRY(c, hipMemcpyAsync(S.h, handles + ch.a, (size_t)ch.cn * sizeof(bhg_handle), hipMemcpyHostToDevice, sc));
+        if (S.e) HIP_TRY(c, hipMemcpyAsync(S.e, expected_crc + ch.a, (size_t)ch.cn * 4, hipMemcpyHostToDevice, sc));
+        HIP_TRY(c, bhg::launch_add_u64(L, reinterpret_cast<uint64_t *>(S.h), ch.cn, 0 - ch.lo, 2));
+        HIP_TRY(c, bhg::launch_decode(L, S.src, ch.hi - ch.lo, S.h, ch.cn, BHG_CODEC_SNAPPY, S.e, S.d, S.off));
+        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, S.off, S.off, ch.cn, S.scan));
+        HIP_TRY(c, hipMemcpyAsync(c->ptot + ch.slot, S.off + ch.cn, 8, hipMemcpyDeviceToHost, sc));
+        HIP_TRY(c, hipEventRecord(c->pev[ch.slot], sc));
+        return BHG_OK;
+    };
+    auto stage_b = [&](Chunk &ch) -> int {
+        const Slot S = slot_of(ch.slot);
+        HIP_TRY(c, hipEventSynchronize(c->pev[ch.slot]));
+        const uint64_t tot = c->ptot[ch.slot];
+        ch.vb = vbase;
+        ch.fit = vbase >= out_vals_cap ? 0 : (tot < out_vals_cap - vbase ? tot : out_vals_cap - vbase);
+        if (int r = ensure_buf(c, &c->pvals[ch.slot], &c->pvals_cap[ch.slot], ch.fit + 80)) return r;
+        ch.mis = mvals ? (((uintptr_t)mvals + vbase) & 15u) : 0u;
+        uint8_t *dv = reinterpret_cast<uint8_t *>(c->pvals[ch.slot]) + ch.mis;
+        const uint64_t ecap = out_vals_cap < vbase + tot ? out_vals_cap : vbase + tot;
+        HIP_TRY(c, bhg::launch_add_u64(L, S.off, (uint64_t)ch.cn + 1, vbase, 1));
+        HIP_TRY(c, bhg::launch_snappy(L, S.src, ch.hi - ch.lo, S.h, ch.cn, S.d, dv - vbase, ecap, S.off, S.list));
+        HIP_TRY(c, hipEventRecord(c->pevb[ch.slot], sc));
+        vbase += tot;
+        return BHG_OK;
+    };
+    auto stage_d = [&](const Chunk &ch) -> int {
+        const Slot S = slot_of(ch.slot);
+        HIP_TRY(c, hipStreamWaitEvent(sd, c->pevb[ch.slot], 0));
+        const uint8_t *dv = reinterpret_cast<const uint8_t *>(c->pvals[ch.slot]) + ch.mis;
+        if (ch.fit && mvals) HIP_TRY(c, bhg::launch_copy_out(Ld, dv, mvals + ch.vb, ch.fit));
+        else if (ch.fit) HIP_TRY(c, hipMemcpyAsync(out_vals + ch.vb, dv, ch.fit, hipMemcpyDeviceToHost, sd));
+        HIP_TRY(c, hipMemcpyAsync(out_val_off + ch.a, S.off, ((size_t)ch.cn + 1) * 8, hipMemcpyDeviceToHost, sd));
+        HIP_TRY(c, hipMemcpyAsync(out_desc + ch.a, S.d, (size_t)ch.cn * sizeof(bhg_desc), hipMemcpyDeviceToHost, sd));
+        HIP_TRY(c, hipEventRecord(c->pevd[ch.slot], sd));
+        dpend[ch.slot] = true;
+        return BHG_OK;
+    };
+    auto next = [&](uint32_t a, int slot) {
+        Chunk ch{};
+        ch.a = a;
+        ch.slot = slot;
+        const uint32_t b = next_chunk(handles, a, n, src_len, kChunkBytes, max_chunk_n, &prev_off, &ch.lo, &ch.hi,
+                                      &unsorted);
+        ch.cn = b - a;
+        return ch;
+    };
+    Chunk cur = next(0, 0);
+    if (int r = stage_a(cur)) return r;
+    for (;;) {
+        if (int r = stage_b(cur)) return r;
+        const uint32_t b = cur.a + cur.cn;
+        Chunk nx{};
+        if (b < n) {
+            nx = next(b, (cur.slot + 1) % bhg_ctx::kPipe);
+            if (int r = stage_a(nx)) return r;
+        }
+        if (int r = stage_d(cur)) return r;
+        if (b >= n) break;
+        cur = nx;
+    }
+    HIP_TRY(c, hipStreamSynchronize(sd));
+    HIP_TRY(c, hipStreamSynchronize(sc));
     return BHG_OK;
 }
 
@@ -460,6 +648,13 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     std::lock_guard<std::mutex> g(c->mu);
+    if (codec == BHG_CODEC_SNAPPY && out_vals) {
+        // sorted handles: the chunked two-stage pipeline (H2D of chunk k + 1 under chunk k's D2H);
+        // otherwise the whole batch below
+        const int r = decode_host_snappy_pipelined(c, src, src_len, handles, n, expected_crc, out_desc, out_vals,
+                                                   out_vals_cap, out_val_off);
+        if (r != -100) return r;
+    }
     if (codec == BHG_CODEC_NONE) {
         // handles in offset order: the chunked pipeline (49.7 GiB/s with src, handles and descriptors
         // pinned, 44 pageable; scripts/lab/e2e_lab.py); from the first handle out of order on (or an

@@ -159,6 +159,10 @@ size_t radix_sort_scratch_bytes(uint32_t n);
 hipError_t launch_radix_sort_pairs(const Launch &L, uint64_t *keys, uint64_t *keys_out, uint32_t *vals,
                                    uint32_t *vals_out, uint32_t n, uint32_t end_bit, void *scratch);
 hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch);
+// p[i * stride] += add (mod 2^64), i in [0, n)
+hipError_t launch_add_u64(const Launch &L, uint64_t *p, uint64_t n, uint64_t add, uint32_t stride);
+// dst (mapped host memory) <- src, n bytes; src == dst mod 16
+hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, uint64_t n);
 
 // bhg_tscan.hip: table data-region scan (count -> scan -> write); first[ntables+1],
 // scan_scratch holds scan_scratch_bytes(ntables).

@@ -4,6 +4,7 @@
 // summed by each workgroup from the chunk sums before it (up to 4,096 chunks = 8M elements;
 // larger inputs scan the sums recursively).  Each workgroup covers 2048 elements (256
 // threads x 8), so 1M sizes need 489 workgroups.
+#include "bhg_device.h"
 #include "bhg_internal.h"
 
 namespace bhg {
@@ -117,6 +118,51 @@ size_t scan_scratch_bytes(uint64_t n) {
 }
 
 // exclusive scan of in[0..n) into out[0..n], out[n] = total.  in may equal out.
+// p[i * stride] += add (mod 2^64) over n entries: the pipelined snappy host path rebases a chunk's
+// scanned value offsets onto the batch (stride 1) and its handles onto the chunk's staged bytes
+// (stride 2: bhg_handle.offset, add = -lo)
+__global__ __launch_bounds__(256) void k_add_u64(uint64_t *p, uint64_t n, uint64_t add, uint32_t stride) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i * stride] += add;
+}
+
+hipError_t launch_add_u64(const Launch &L, uint64_t *p, uint64_t n, uint64_t add, uint32_t stride) {
+    if (n == 0 || add == 0) return hipSuccess;
+    uint64_t grid = (n + 255) / 256;
+    const uint64_t cap = (uint64_t)L.num_cus * 4;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(k_add_u64, dim3((uint32_t)grid), dim3(256), 0, L.stream, p, n, add, stride);
+    return hipGetLastError();
+}
+
+// dst <- src, n bytes, dst in page-locked host memory mapped into the device (the pipelined
+// snappy host path's values: a copy kernel writes them over PCIe at the link rate, where a
+// D2H copy may take a DMA engine that runs at half of it, scripts/lab/e2e_snappy/).  The
+// caller places src so that src and dst agree mod 16: the bulk moves in aligned 16-B units,
+// only a head and a tail of under 16 bytes go bytewise.
+__global__ __launch_bounds__(256) void k_copy_out(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                  uint64_t n) {
+    const uint64_t mis = (16u - ((uint64_t)dst & 15u)) & 15u;
+    const uint64_t head = mis < n ? mis : n;
+    const uint64_t nv = (n - head) / 16, t0 = head + nv * 16;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src + head);
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(dst + head);
+    for (uint64_t i = tid; i < nv; i += stride) d4[i] = s4[i];
+    if (tid < head) dst[tid] = src[tid];
+    if (tid < n - t0) dst[t0 + tid] = src[t0 + tid];
+}
+
+hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, uint64_t n) {
+    if (n == 0) return hipSuccess;
+    uint64_t grid = (n / 16 + 255) / 256;
+    const uint64_t cap = (uint64_t)L.num_cus * 2;
+    if (grid > cap) grid = cap;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(k_copy_out, dim3((uint32_t)grid), dim3(256), 0, L.stream, src, dst, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch) {
     if (n == 0) {
         return hipMemsetAsync(out, 0, sizeof(uint64_t), L.stream);

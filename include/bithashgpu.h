@@ -167,10 +167,14 @@ int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const b
  * unsorted handles a page-locked + mapped src (bhg_host_register,
  * bhg_malloc_host) is decoded in place over PCIe with no staging copy
  * (out_desc / handles / expected_crc used in place too when mapped);
- * otherwise src is copied whole first.  SNAPPY always stages src in HBM.
- * SNAPPY: the device value
- * buffer is sized from the scanned total (not from out_vals_cap); out_vals
- * NULL returns only out_val_off (the sizing pass). */
+ * otherwise src is copied whole first.  SNAPPY with handles sorted by offset
+ * (every record within 64 MiB) and out_vals given: pipelined in <= 64 MiB src
+ * chunks on two streams, chunk k + 1's H2D under chunk k's values, offsets and
+ * descriptors coming back; a page-locked + mapped out_vals is written by a copy
+ * kernel (pin src and out_vals for the link rate).  Otherwise SNAPPY stages src
+ * whole in HBM.  SNAPPY: device value buffers are sized from the scanned totals
+ * (not from out_vals_cap); out_vals NULL returns only out_val_off (the sizing
+ * pass). */
 int bhg_decode_batch_host(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_handle *handles,
                           uint32_t n, int codec, const uint32_t *expected_crc, bhg_desc *out_desc,
                           uint8_t *out_vals, uint64_t out_vals_cap, uint64_t *out_val_off);

@@ -746,3 +746,67 @@ def test_fuzz_corrupt_records(codec, seed):
                 assert gv[a:b].tobytes() == ev[a:b].tobytes(), (i, int(exp["status"][i]))
         st = np.bincount(exp["status"], minlength=16)
         assert st[0] > n // 2 and (st[1:] > 0).sum() >= 3, st   # most OK, several failure kinds hit
+
+
+@pytest.mark.parametrize("chunk,cap_at,big,pin", [(4096, None, False, False), (1 << 16, None, False, False),
+                                                  (1 << 16, 1900, False, False), (1 << 16, 2600, False, False),
+                                                  (4096, None, True, False), (1 << 16, None, False, True),
+                                                  (4096, 2600, False, True)])
+def test_host_snappy_pipelined(chunk, cap_at, big, pin, monkeypatch):
+    """bhg_decode_batch_host, SnappyCompressor, handles sorted by offset: the
+    two-stage chunked pipeline (offsets rebased per chunk, chunk k + 1's H2D under
+    chunk k's D2H) equals the restatement: descriptors, value offsets and
+    values, with empty values, a zero-length handle, a handle running past src,
+    flipped expected CRCs, a caller cap that ends inside a later chunk (the
+    same SNAPPY_TOO_LARGE verdicts as the device path, empty values past it
+    included), and records larger than a chunk (the whole-batch fallback).
+    pin: source, values and descriptors page-locked (bhg_host_register), so the
+    values go back by the copy kernel into the mapped buffer, at every offset
+    mod 16 the chunk bases fall on."""
+    from bitalosdb_amd.codec import BithashCodec
+    monkeypatch.setenv("BHG_HOST_CHUNK_BYTES", str(chunk))
+    c = BithashCodec(0)
+    rng = random.Random(chunk + (cap_at or 0) + big)
+    sizes = [0, 1, 64, 1024, 3000] + ([20000] if big else [])
+    specs = [(rand_bytes(rng, rng.choice([0, 7, 32])), compressible(rng, rng.choice(sizes)), 3) for _ in range(3000)]
+    src, h = make_records(rng, specs, gap_max=3, codec=1)
+    h = h.copy()
+    h["length"][100] = 0                       # ErrBhIllegalBlockLength
+    h["length"][2999] += 9                     # runs past src: INCOMPLETE
+    exp0, _, _ = O.decode_batch(src, h, codec=1)
+    expected = exp0["crc"].copy()
+    expected[5::97] ^= 1
+    exp, ev, eo = O.decode_batch(src, h, codec=1, expected_crc=expected)
+    buf = np.frombuffer(src, np.uint8).copy()
+    cap = None if cap_at is None else int(eo[cap_at]) + 5
+    kw = {}
+    pinned = []
+    if pin:
+        from bitalosdb_amd.codec import DESC_DT
+        kw = {"out_vals": np.full(int(eo[-1]) + 100 if cap is None else cap, 0xEE, dtype=np.uint8),
+              "out_desc": np.empty(len(h), dtype=DESC_DT)}
+        pinned = [buf, kw["out_vals"], kw["out_desc"]]
+        for a in pinned:
+            c.host_register(a)
+    try:
+        got, gv, go = c.decode_host(buf, h, compressor=1, expected_crc=expected, out_vals_cap=cap, **kw)
+    finally:
+        for a in pinned[::-1]:
+            c.host_unregister(a)
+    if pin and cap is None:
+        assert (kw["out_vals"][int(eo[-1]):] == 0xEE).all()          # nothing written past the values
+    if cap_at is None:
+        assert_desc_equal(got, exp)
+        assert np.array_equal(go, eo) and gv.tobytes() == ev[:int(eo[-1])].tobytes()
+        assert (got["status"] == O.CRC_MISMATCH).sum() > 0
+    else:
+        assert np.array_equal(go, eo)
+        ends = eo[1:]
+        live = (exp["status"] == 0) | (exp["status"] == O.CRC_MISMATCH)
+        assert (got["status"][live & (ends > cap)] == O.SNAPPY_TOO_LARGE).all()
+        assert ((ends > cap) & live & (exp["val_len"] == 0)).sum() > 0     # empty values past the cap
+        ok = ~(live & (ends > cap))
+        for f in FIELDS:
+            assert np.array_equal(got[f][ok], exp[f][ok]), f
+        assert gv[:int(eo[cap_at])].tobytes() == ev[:int(eo[cap_at])].tobytes()
+    c.close()
