@@ -806,7 +806,8 @@ def c3_measure(a, world, rank, local, dev, codec, gen, extras):
                            "note": "host src (%.2f GB) + handles + expected CRCs -> descriptors, value offsets and "
                                    "%.2f GB of decoded values in host memory: 64 MiB src chunks, chunk k + 1's H2D "
                                    "under chunk k's values going back (a copy kernel into the mapped out_vals when "
-                                   "it is page-locked, else D2H copies), caller-owned output buffers reused.  value: "
+                                   "it is page-locked, else into page-locked staging that host threads copy on), "
+                                   "caller-owned output buffers reused.  value: "
                                    "all host buffers page-locked (bhg_host_register); pageable also given"
                                    % (host_src.size / 1e9, n * 1024 / 1e9)}
         out["valid"] = bool(out["valid"] and host_ok)

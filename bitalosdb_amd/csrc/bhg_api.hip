@@ -11,12 +11,82 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 
 #include <vector>
 
 #include "bhg_crc_tables.h"
 #include "bhg_internal.h"
+
+// Host threads that copy page-locked staging buffers into pageable caller buffers (the pipelined
+// snappy host path with a pageable out_vals): one job at a time, every thread taking an equal
+// share of each segment.  submit() returns at once; wait() blocks until the job is done.
+struct HostCopyPool {
+    struct Seg {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+    explicit HostCopyPool(int nthreads) : nt(nthreads) {
+        for (int t = 0; t < nthreads; t++) th.emplace_back([this, t] { worker(t); });
+    }
+    ~HostCopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+    void submit(const std::vector<Seg> &s) {
+        wait();
+        {
+            std::lock_guard<std::mutex> lk(m);
+            segs = s;
+            pending = nt;
+            gen++;
+        }
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(m);
+        done.wait(lk, [&] { return pending == 0; });
+    }
+
+  private:
+    void worker(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::vector<Seg> job;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                job = segs;
+            }
+            for (const Seg &g : job) {
+                const size_t per = ((g.n + nt - 1) / nt + 63) & ~(size_t)63;
+                const size_t a = (size_t)id * per, b = a + per < g.n ? a + per : g.n;
+                if (a < b) memcpy(g.dst + a, g.src + a, b - a);
+            }
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (--pending == 0) done.notify_all();
+            }
+        }
+    }
+    const int nt;
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done;
+    std::vector<Seg> segs;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+};
 
 struct bhg_ctx {
     int device;
@@ -44,6 +114,12 @@ struct bhg_ctx {
     hipEvent_t pev[kPipe] = {nullptr, nullptr, nullptr};   // chunk total in ptot
     hipEvent_t pevb[kPipe] = {nullptr, nullptr, nullptr};  // chunk values decoded
     hipEvent_t pevd[kPipe] = {nullptr, nullptr, nullptr};  // chunk copied back (slot free)
+    // ... with a pageable out_vals: page-locked staging per slot (values, offsets, descriptors,
+    // written by copy kernels) and the host threads that copy it on into the caller's buffers
+    uint8_t *pstage[kPipe] = {nullptr, nullptr, nullptr};
+    uint8_t *pstage_dev[kPipe] = {nullptr, nullptr, nullptr};  // its device address
+    size_t pstage_cap[kPipe] = {0, 0, 0};
+    HostCopyPool *hpool = nullptr;
 };
 
 namespace {
@@ -208,6 +284,9 @@ void bhg_destroy(bhg_ctx *c) {
         if (c->pevd[k]) (void)hipEventDestroy(c->pevd[k]);
     }
     if (c->ptot) (void)hipHostFree(c->ptot);
+    delete c->hpool;  // joins its threads (idle: every host call waits for its copies)
+    for (int k = 0; k < bhg_ctx::kPipe; k++)
+        if (c->pstage[k]) (void)hipHostFree(c->pstage[k]);
     if (c->h_src) (void)hipFree(c->h_src);
     if (c->h_aux) (void)hipFree(c->h_aux);
     if (c->h_vals) (void)hipFree(c->h_vals);
@@ -444,8 +523,12 @@ const void *mapped_device_ptr(const void *p);
 //   D (copy stream, after pevb): values, offsets and descriptors back to the host (event pevd,
 //     which A of the chunk that next takes the slot waits for).  Values into a page-locked,
 //     mapped out_vals go by a copy kernel (k_copy_out: the link rate; a D2H copy may get a DMA
-//     engine that runs at half of it), else by a D2H copy; the slot buffer then holds them at
-//     the host address's offset mod 16.
+//     engine that runs at half of it), the slot buffer then holding them at the host address's
+//     offset mod 16; offsets and descriptors by D2H copies.  With a pageable out_vals, copy
+//     kernels write values, offsets and descriptors into the slot's page-locked staging
+//     buffer, and host threads (HostCopyPool) copy chunk k - 1's staging into the caller's
+//     buffers while the host thread issues chunk k + 1 (a pageable D2H copy would hold the
+//     host thread for its whole length).
 // The host issues B(k), A(k + 1), D(k) in that order, so an H2D is always queued before the
 // D2H it should overlap (a D2H call may return only when its copy is done).  Rebasing keeps
 // every status: in-bounds records lie in [lo, hi); the others stay past the end (the offsets
@@ -512,6 +595,17 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
     bhg::Launch Ld = L;
     Ld.stream = sd;
     uint8_t *mvals = const_cast<uint8_t *>(static_cast<const uint8_t *>(mapped_device_ptr(out_vals)));
+    const bool staged = mvals == nullptr;
+    if (staged && !c->hpool) {
+        const unsigned hc = std::thread::hardware_concurrency();
+        c->hpool = new HostCopyPool(hc < 2 ? 2 : hc > 8 ? 8 : (int)hc);
+    }
+    struct PoolWait {  // no return leaves a host copy running into the caller's buffers
+        HostCopyPool *p;
+        ~PoolWait() {
+            if (p) p->wait();
+        }
+    } pool_wait{staged ? c->hpool : nullptr};
     bool dpend[bhg_ctx::kPipe] = {false, false, false};  // the slot's last D2H has an event to wait for
     uint64_t vbase = 0;                                   // the batch offset of the next chunk's first value
     uint64_t prev_off = 0;
@@ -545,9 +639,40 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
         vbase += tot;
         return BHG_OK;
     };
+    // staging layout of a slot: values (fit bytes), offsets, descriptors
+    auto stage_offs = [&](const Chunk &ch, size_t &o_off, size_t &o_desc) {
+        o_off = al(ch.fit + 16);
+        o_desc = o_off + al(((size_t)ch.cn + 1) * 8);
+        return o_desc + al((size_t)ch.cn * sizeof(bhg_desc));
+    };
     auto stage_d = [&](const Chunk &ch) -> int {
         const Slot S = slot_of(ch.slot);
         HIP_TRY(c, hipStreamWaitEvent(sd, c->pevb[ch.slot], 0));
+        if (staged) {
+            size_t o_off, o_desc;
+            const size_t need_s = stage_offs(ch, o_off, o_desc);
+            if (need_s > c->pstage_cap[ch.slot]) {  // free: its last chunk was copied on (see drain)
+                if (c->pstage[ch.slot]) HIP_TRY(c, hipHostFree(c->pstage[ch.slot]));
+                c->pstage[ch.slot] = nullptr;
+                c->pstage_cap[ch.slot] = 0;
+                const size_t sz = need_s + need_s / 4 + 4096;
+                HIP_TRY(c, hipHostMalloc(reinterpret_cast<void **>(&c->pstage[ch.slot]), sz, hipHostMallocMapped));
+                c->pstage_cap[ch.slot] = sz;
+                void *dp = nullptr;
+                HIP_TRY(c, hipHostGetDevicePointer(&dp, c->pstage[ch.slot], 0));
+                c->pstage_dev[ch.slot] = static_cast<uint8_t *>(dp);
+            }
+            uint8_t *sdv = c->pstage_dev[ch.slot];
+            const uint8_t *dv = reinterpret_cast<const uint8_t *>(c->pvals[ch.slot]) + ch.mis;
+            HIP_TRY(c, bhg::launch_copy_out(Ld, dv, sdv, ch.fit));
+            HIP_TRY(c, bhg::launch_copy_out(Ld, reinterpret_cast<const uint8_t *>(S.off), sdv + o_off,
+                                            ((size_t)ch.cn + 1) * 8));
+            HIP_TRY(c, bhg::launch_copy_out(Ld, reinterpret_cast<const uint8_t *>(S.d), sdv + o_desc,
+                                            (size_t)ch.cn * sizeof(bhg_desc)));
+            HIP_TRY(c, hipEventRecord(c->pevd[ch.slot], sd));
+            dpend[ch.slot] = true;
+            return BHG_OK;
+        }
         const uint8_t *dv = reinterpret_cast<const uint8_t *>(c->pvals[ch.slot]) + ch.mis;
         if (ch.fit && mvals) HIP_TRY(c, bhg::launch_copy_out(Ld, dv, mvals + ch.vb, ch.fit));
         else if (ch.fit) HIP_TRY(c, hipMemcpyAsync(out_vals + ch.vb, dv, ch.fit, hipMemcpyDeviceToHost, sd));
@@ -566,7 +691,21 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
         ch.cn = b - a;
         return ch;
     };
-    Chunk cur = next(0, 0);
+    // staged: chunk ch's staging -> the caller's buffers on the host threads (the offsets' last
+    // entry only from the batch's last chunk: the next chunk writes the same word)
+    auto drain = [&](const Chunk &ch) -> int {
+        HIP_TRY(c, hipEventSynchronize(c->pevd[ch.slot]));
+        size_t o_off, o_desc;
+        stage_offs(ch, o_off, o_desc);
+        const uint8_t *st = c->pstage[ch.slot];
+        const bool last = ch.a + ch.cn >= n;
+        c->hpool->submit({{out_vals + ch.vb, st, ch.fit},
+                          {reinterpret_cast<uint8_t *>(out_val_off + ch.a), st + o_off, ((size_t)ch.cn + last) * 8},
+                          {reinterpret_cast<uint8_t *>(out_desc + ch.a), st + o_desc, (size_t)ch.cn * sizeof(bhg_desc)}});
+        return BHG_OK;
+    };
+    Chunk cur = next(0, 0), prev{};
+    bool have_prev = false;
     if (int r = stage_a(cur)) return r;
     for (;;) {
         if (int r = stage_b(cur)) return r;
@@ -577,9 +716,19 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
             if (int r = stage_a(nx)) return r;
         }
         if (int r = stage_d(cur)) return r;
+        if (staged) {
+            // a slot's staging is rewritten by stage D three chunks on: submit() first waits for the
+            // previous host copy, so chunk k - 3's copy is done before chunk k's kernels are queued
+            if (have_prev)
+                if (int r = drain(prev)) return r;
+            prev = cur;
+            have_prev = true;
+        }
         if (b >= n) break;
         cur = nx;
     }
+    if (staged && have_prev)
+        if (int r = drain(prev)) return r;
     HIP_TRY(c, hipStreamSynchronize(sd));
     HIP_TRY(c, hipStreamSynchronize(sc));
     return BHG_OK;

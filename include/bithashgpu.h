@@ -171,7 +171,8 @@ int bhg_decode_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const b
  * (every record within 64 MiB) and out_vals given: pipelined in <= 64 MiB src
  * chunks on two streams, chunk k + 1's H2D under chunk k's values, offsets and
  * descriptors coming back; a page-locked + mapped out_vals is written by a copy
- * kernel (pin src and out_vals for the link rate).  Otherwise SNAPPY stages src
+ * kernel, a pageable one through page-locked staging and host copy threads
+ * (pin src and out_vals for the link rate).  Otherwise SNAPPY stages src
  * whole in HBM.  SNAPPY: device value buffers are sized from the scanned totals
  * (not from out_vals_cap); out_vals NULL returns only out_val_off (the sizing
  * pass). */

@@ -3,8 +3,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/e2e_snappy
 mkdir -p $O
-for cb in 16777216 33554432 67108864 134217728; do
-  echo "chunk $cb"
-  BHG_HOST_CHUNK_BYTES=$cb timeout -k 10 200 python3 -u scripts/lab/e2e_snappy/e2e_trace.py > $O/e2e_cb$cb.txt 2>&1 || exit 1
-  grep call $O/e2e_cb$cb.txt | tail -2
-done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_decode.py tests/test_c_client.py -m gpu -x -v -k "host or client" --timeout 120 --timeout-method thread > $O/pytest_host.txt 2>&1; rc=$?
+tail -3 $O/pytest_host.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --config c3 --no-secondary --no-traffic --no-cpu > $O/bench_c3_staged.json 2> $O/bench_c3_staged.err || exit 1
+python -c "
+import json; d=json.load(open('$O/bench_c3_staged.json')); print(d['value'], json.dumps(d.get('e2e_host')))"
