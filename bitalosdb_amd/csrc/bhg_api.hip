@@ -30,21 +30,20 @@ struct HostCopyPool {
         size_t n;
     };
     explicit HostCopyPool(int nthreads) : nt(nthreads) {
-        for (int t = 0; t < nthreads; t++) th.emplace_back([this, t] { worker(t); });
-    }
-    ~HostCopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(m);
-            stop = true;
+        segs.reserve(4);  // submit() then never allocates
+        try {
+            for (int t = 0; t < nthreads; t++) th.emplace_back([this, t] { worker(t); });
+        } catch (...) {  // the threads already started are stopped before the exception leaves
+            shutdown();
+            throw;
         }
-        cv.notify_all();
-        for (auto &t : th) t.join();
     }
-    void submit(const std::vector<Seg> &s) {
+    ~HostCopyPool() { shutdown(); }
+    void submit(std::initializer_list<Seg> s) {
         wait();
         {
             std::lock_guard<std::mutex> lk(m);
-            segs = s;
+            segs.assign(s);
             pending = nt;
             gen++;
         }
@@ -56,6 +55,15 @@ struct HostCopyPool {
     }
 
   private:
+    void shutdown() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+        th.clear();
+    }
     void worker(int id) {
         uint64_t seen = 0;
         for (;;) {
@@ -598,7 +606,12 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
     const bool staged = mvals == nullptr;
     if (staged && !c->hpool) {
         const unsigned hc = std::thread::hardware_concurrency();
-        c->hpool = new HostCopyPool(hc < 2 ? 2 : hc > 8 ? 8 : (int)hc);
+        try {
+            c->hpool = new HostCopyPool(hc < 2 ? 2 : hc > 8 ? 8 : (int)hc);
+        } catch (...) {  // no exception crosses the C ABI
+            set_err(c, "host copy threads could not be started");
+            return BHG_ENOMEM;
+        }
     }
     struct PoolWait {  // no return leaves a host copy running into the caller's buffers
         HostCopyPool *p;
