@@ -156,7 +156,9 @@ __global__ __launch_bounds__(256) void k_copy_out(const uint8_t *__restrict__ sr
 hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, uint64_t n) {
     if (n == 0) return hipSuccess;
     uint64_t grid = (n / 16 + 255) / 256;
-    const uint64_t cap = (uint64_t)L.num_cus * 2;
+    // one workgroup per 4 CUs: the link, not the grid, sets the rate (64 .. 1,024 workgroups
+    // measured within 1 % on the snappy host path, profiles/r4/e2e_snappy/copy_out_grid.txt)
+    const uint64_t cap = (uint64_t)L.num_cus / 4;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(k_copy_out, dim3((uint32_t)grid), dim3(256), 0, L.stream, src, dst, n);
