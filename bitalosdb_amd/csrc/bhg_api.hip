@@ -859,13 +859,17 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
         HIP_TRY(c, hipMemcpyAsync(out_val_off, doff, ob, hipMemcpyDeviceToHost, s));
         HIP_TRY(c, hipStreamSynchronize(s));
         if (out_vals) {
-            // the device value buffer is sized from the scanned total, capped by what the caller can take
+            // the device value buffer is sized from the scanned total, capped by what the caller can take;
+            // a page-locked + mapped out_vals is written by the copy kernel (the link rate, see
+            // decode_host_snappy_pipelined), the values then placed at its address's offset mod 16
             uint64_t total = out_val_off[n];
             if (total > out_vals_cap) total = out_vals_cap;
-            if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 64)) return r;
-            uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals);
+            if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 80)) return r;
+            uint8_t *mv = const_cast<uint8_t *>(static_cast<const uint8_t *>(mapped_device_ptr(out_vals)));
+            uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals) + (mv ? ((uintptr_t)mv & 15u) : 0u);
             HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dlist));
-            if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
+            if (total && mv) HIP_TRY(c, bhg::launch_copy_out(L, dv, mv, total));
+            else if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
         }
     }
     HIP_TRY(c, hipMemcpyAsync(out_desc, dd, db, hipMemcpyDeviceToHost, s));

@@ -1,12 +1,11 @@
 #!/bin/bash
-# k_copy_out grid sweep (workgroups per 4 CUs) on the pinned snappy e2e path
+# whole-batch snappy host path (unsorted handles) with the copy kernel: tests, then timing
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/e2e_snappy
 mkdir -p $O
-: > $O/copy_out_grid.txt
-for v in co1 co2 co4 co8 co16; do
-  echo "== $v" >> $O/copy_out_grid.txt
-  BHG_LIB_PATH=$GRAFT_REPO_ROOT/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 200 python3 -u scripts/lab/e2e_snappy/e2e_trace.py >> $O/copy_out_grid.txt 2>&1 || exit 1
-done
-grep "==\|call [23]" $O/copy_out_grid.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_decode.py tests/test_c_client.py -m gpu -x -v -k "host or client" --timeout 120 --timeout-method thread > $O/pytest_host3.txt 2>&1; rc=$?
+tail -3 $O/pytest_host3.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 -u scripts/lab/e2e_snappy/e2e_trace.py shuffle > $O/e2e_unsorted.txt 2>&1 || exit 1
+grep call $O/e2e_unsorted.txt

@@ -810,3 +810,37 @@ def test_host_snappy_pipelined(chunk, cap_at, big, pin, monkeypatch):
             assert np.array_equal(got[f][ok], exp[f][ok]), f
         assert gv[:int(eo[cap_at])].tobytes() == ev[:int(eo[cap_at])].tobytes()
     c.close()
+
+
+@pytest.mark.parametrize("pin", [False, True])
+def test_host_snappy_unsorted(codec, pin):
+    """bhg_decode_batch_host, SnappyCompressor, handles in random order (the
+    whole-batch path): descriptors, value offsets (in handle order) and values
+    equal the restatement; with out_vals page-locked the values go back by the
+    copy kernel into the mapped buffer, and nothing past them is written."""
+    from bitalosdb_amd.codec import DESC_DT
+    rng = random.Random(404)
+    specs = [(rand_bytes(rng, rng.choice([0, 7, 32])), compressible(rng, rng.choice([0, 1, 64, 1024, 3000])), 2)
+             for _ in range(2500)]
+    src, h = make_records(rng, specs, gap_max=3, codec=1)
+    h = h[np.random.default_rng(17).permutation(len(h))].copy()
+    h["length"][7] = 0                         # ErrBhIllegalBlockLength
+    exp0, _, _ = O.decode_batch(src, h, codec=1)
+    expected = exp0["crc"].copy()
+    expected[3::89] ^= 1
+    exp, ev, eo = O.decode_batch(src, h, codec=1, expected_crc=expected)
+    buf = np.frombuffer(src, np.uint8).copy()
+    vals = np.full(int(eo[-1]) + 100, 0xEE, dtype=np.uint8)
+    desc = np.empty(len(h), dtype=DESC_DT)
+    pinned = [buf, vals, desc] if pin else []
+    for a in pinned:
+        codec.host_register(a)
+    try:
+        got, gv, go = codec.decode_host(buf, h, compressor=1, expected_crc=expected, out_desc=desc, out_vals=vals)
+    finally:
+        for a in pinned[::-1]:
+            codec.host_unregister(a)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(go, eo) and gv.tobytes() == ev[:int(eo[-1])].tobytes()
+    assert (vals[int(eo[-1]):] == 0xEE).all()
+    assert (got["status"] == O.CRC_MISMATCH).sum() > 0
