@@ -1,7 +1,7 @@
 """Lab: the snappy end-to-end host path (bhg_decode_batch_host, pinned buffers) on the c3
 workload (1M dict-value blocks), timed per call; run under rocprofv3 --kernel-trace
 --memory-copy-trace to see how the chunk copies and kernels overlap.  argv[1] == "shuffle":
-handles in random order (the whole-batch path)."""
+handles in random order (the whole-batch path); "pageable": no host buffer page-locked."""
 import os
 import sys
 import time
@@ -19,13 +19,13 @@ n = 1 << 20
 val_lens = torch.full((n,), 1024, dtype=torch.int64, device=dev)
 src, h, meta, enc = bench._encode_tables(codec, n, val_lens, dev, bench.synth_seed(0), 1, "dict")
 ecrc = enc[-1].crc.cpu().numpy().view(np.uint32).copy()
-if len(sys.argv) > 1 and sys.argv[1] == "shuffle":
+if "shuffle" in sys.argv[1:]:
     perm = np.random.default_rng(3).permutation(n)
     h, ecrc = h[perm].copy(), ecrc[perm].copy()
 host_src = src.cpu().numpy()
 desc = np.empty(n, dtype=DESC_DT)
 vals = np.empty(n * 1024 + 64, dtype=np.uint8)
-bufs = (host_src, desc, vals, h, ecrc)
+bufs = () if "pageable" in sys.argv[1:] else (host_src, desc, vals, h, ecrc)
 for b in bufs:
     codec.host_register(b)
 disk = float(h["length"].astype(np.float64).sum())

@@ -1,11 +1,12 @@
 #!/bin/bash
-# whole-batch snappy host path (unsorted handles) with the copy kernel: tests, then timing
+# host copy threads for pageable snappy outputs: 4 / 8 / 12 / 16
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/e2e_snappy
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_decode.py tests/test_c_client.py -m gpu -x -v -k "host or client" --timeout 120 --timeout-method thread > $O/pytest_host3.txt 2>&1; rc=$?
-tail -3 $O/pytest_host3.txt
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 -u scripts/lab/e2e_snappy/e2e_trace.py shuffle > $O/e2e_unsorted.txt 2>&1 || exit 1
-grep call $O/e2e_unsorted.txt
+: > $O/hpool_threads.txt
+for v in hp4 hp8 hp12 hp16; do
+  echo "== $v" >> $O/hpool_threads.txt
+  BHG_LIB_PATH=$GRAFT_REPO_ROOT/scripts/lab/libvar/$v/libbithashgpu.so timeout -k 10 200 python3 -u scripts/lab/e2e_snappy/e2e_trace.py pageable >> $O/hpool_threads.txt 2>&1 || exit 1
+done
+grep "==\|call" $O/hpool_threads.txt
