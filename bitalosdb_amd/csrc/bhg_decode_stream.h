@@ -96,6 +96,24 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
     __shared__ __attribute__((aligned(16))) uint32_t Zf[1024];
     __shared__ __attribute__((aligned(16))) uint32_t Zs[6 * 1024];
     __shared__ uint32_t E[128];
+    const Crc4Perm crc(T);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint64_t lo4 = base & ~3ull, hi4 = (end - 1) & ~3ull;  // first / last dword holding source bytes
+    const uint64_t safe = (base + 3) & ~3ull;                     // stand-in load address (interior tiles)
+    const uint64_t lowmask = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t tstride = gridDim.x * WPB;
+    // wave-major tile index: waves that take one tile more than the others are spread over every CU
+    uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    // the next tile's handles and the expected CRCs are loaded with no branch around them
+    // (index clamped; see fetch below for why)
+    auto hidx = [&](uint32_t t) { const uint32_t x = t * 64 + lane; return x < n ? x : n - 1; };
+    const uint32_t *ecp = expected_crc != nullptr ? expected_crc : gtab;
+    const uint32_t emask = expected_crc != nullptr ? 0xffffffffu : 0u;
+    bhg_handle hn = handles[hidx(tile < ntiles ? tile : 0)];
+    // (the first tile's handles are in flight while the LDS tables are built: C3 step 0.9383 vs
+    // 0.9406 ms, 3 alternating runs each, profiles/r4/early_lab_stream_handles.txt)
     Crc4Perm::fill(T);
     if (!(KO & 128)) {  // all loads issued before the first LDS store (one memory round trip)
         constexpr uint32_t NT = 64 * WPB, NZ = (7 * 1024 + NT - 1) / NT;
@@ -115,22 +133,6 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         if (threadIdx.x < 128) E[threadIdx.x] = e;
     }
     __syncthreads();
-    const Crc4Perm crc(T);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint64_t lo4 = base & ~3ull, hi4 = (end - 1) & ~3ull;  // first / last dword holding source bytes
-    const uint64_t safe = (base + 3) & ~3ull;                     // stand-in load address (interior tiles)
-    const uint64_t lowmask = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-    const uint32_t ntiles = (n + 63) / 64;
-    const uint32_t tstride = gridDim.x * WPB;
-    // wave-major tile index: waves that take one tile more than the others are spread over every CU
-    uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    // the next tile's handles and the expected CRCs are loaded with no branch around them
-    // (index clamped; see fetch below for why)
-    auto hidx = [&](uint32_t t) { const uint32_t x = t * 64 + lane; return x < n ? x : n - 1; };
-    const uint32_t *ecp = expected_crc != nullptr ? expected_crc : gtab;
-    const uint32_t emask = expected_crc != nullptr ? 0xffffffffu : 0u;
-    bhg_handle hn = handles[hidx(tile < ntiles ? tile : 0)];
     for (; tile < ntiles; tile += tstride) {
         const bhg_handle h = hn;
         const uint32_t i = tile * 64 + lane;
