@@ -105,7 +105,7 @@ def lib():
             "bhg_host_unregister": (I, [P, P]),
             "bhg_get_batch": (I, [P, P, U64, P, U32, P, P, P, P, U32, P, P, P]),
             "bhg_writer_index_build": (I, [P, P, U32, P, P, P]),
-            "bhg_bithash_get_batch": (I, [P, P, U64, P, U32, P, U32, P, P, U32, P, P, P, P, U32, P, P, P]),
+            "bhg_bithash_get_batch": (I, [P, P, U64, P, U32, P, U32, P, P, U32, P, P, P, P, I, U32, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

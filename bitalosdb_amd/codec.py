@@ -250,9 +250,11 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_writer_index_build")
         return srt, skh
 
-    def bithash_get(self, src_t, writers, tables, fn_map, fn_table, keys, file_nums, khash=None):
+    def bithash_get(self, src_t, writers, tables, fn_map, fn_table, keys, file_nums, khash=None, compressor=0):
         """Bithash.Get over a batch (bhg_bithash_get_batch): the open writer of each query's
-        fileNum first (Writer.Get), then GetFileNumMap and Reader.Get on the mapped table.
+        fileNum first (Writer.Get; final only when its read would return a value: the record
+        checks and, for compressor 1, the snappy stream), then GetFileNumMap and Reader.Get on
+        the mapped table.
 
         writers: WRITER_INDEX_DT array (device pointers: record handles, writer_index outputs);
         tables: TABLE_DT; fn_map / fn_table: per fileNum (dst fileNum or 0 / table index or
@@ -282,7 +284,8 @@ class BithashCodec:
             out_s = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         rc = self.L.bhg_bithash_get_batch(self.ctx, _ptr(src_t), src_t.numel(), _ptr(w_t), len(writers), _ptr(tab_t),
                                           len(tables), _ptr(fm_t), _ptr(ft_t), len(fn_map), _ptr(kb_t), _ptr(ko_t),
-                                          _ptr(fn_t), _ptr(kh_t), n, _ptr(out_h), _ptr(out_s), self._stream())
+                                          _ptr(fn_t), _ptr(kh_t), int(compressor), n, _ptr(out_h), _ptr(out_s),
+                                          self._stream())
         B.check(self.ctx, rc, "bhg_bithash_get_batch")
         return out_h[:2 * n], out_s[:n]
 

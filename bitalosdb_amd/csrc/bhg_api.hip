@@ -913,9 +913,13 @@ int bhg_writer_index_build(bhg_ctx *c, const uint32_t *khash, uint32_t n, uint32
 int bhg_bithash_get_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
                           uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
                           const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
-                          const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_handles,
-                          uint32_t *out_status, void *stream) {
+                          const uint32_t *file_nums, const uint32_t *khash, int codec, uint32_t n,
+                          bhg_handle *out_handles, uint32_t *out_status, void *stream) {
     if (!c) return BHG_EINVAL;
+    if (codec != BHG_CODEC_NONE && codec != BHG_CODEC_SNAPPY) {
+        set_err(c, "unknown codec");
+        return BHG_EINVAL;
+    }
     if (n == 0) return BHG_OK;
     if (!key_off || !file_nums || !out_handles || !out_status || (!src && src_len) || !keys ||
         (nwriters && !writers) || (ntables && !tables) || (fn_count && (!fn_map || !fn_table))) {
@@ -924,8 +928,8 @@ int bhg_bithash_get_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     }
     if (int r = set_device(c)) return r;
     HIP_TRY(c, bhg::launch_bithash_get(launch_of(c, stream), src, src_len, writers, nwriters, tables, ntables, fn_map,
-                                       fn_table, fn_count, keys, key_off, file_nums, khash, n, out_handles,
-                                       out_status));
+                                       fn_table, fn_count, keys, key_off, file_nums, khash, codec, n,
+                                       out_handles, out_status));
     return BHG_OK;
 }
 

@@ -272,8 +272,79 @@ __device__ bool writer_lookup(uint64_t base, uint64_t end, const bhg_writer_inde
     return true;
 }
 
-// Bithash.Get (bithash.go:101-119): the open writer of file_num first (Writer.Get), then
-// GetFileNumMap(fn) (:264-273; 0 -> ErrBhFileNumZero) and Reader.Get on that table
+// golang/snappy v0.0.4 Decode's error checks (decode.go decodedLen, decode_other.go decode) over
+// the stream [p, p + n) without producing output: true iff Decode returns err == nil, with the
+// decoded length in dlen.  Lane-serial byte loads: it runs only on open-writer hits.
+__device__ bool snappy_stream_ok(uint64_t p, uint64_t n, uint64_t &dlen) {
+    uint64_t x = 0, hdr = 0;
+    uint32_t sh = 0;
+    bool ok = false;
+    for (uint64_t i = 0; i < n && i < 10; i++) {  // binary.Uvarint; > 0xffffffff -> ErrTooLarge
+        const uint32_t b = ld8(p + i);
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return false;
+            x |= (uint64_t)b << sh;
+            ok = x <= 0xffffffffull;
+            hdr = i + 1;
+            break;
+        }
+        x |= (uint64_t)(b & 0x7f) << sh;
+        sh += 7;
+    }
+    if (!ok) return false;
+    dlen = x;
+    const uint64_t s0 = p + hdr, se = p + n;
+    uint64_t s = s0, d = 0;
+    while (s < se) {
+        const uint32_t tag = ld8(s);
+        uint64_t length, offset = 0;
+        if ((tag & 3) == 0) {  // literal
+            uint32_t v = tag >> 2, nb = v < 60 ? 0u : v - 59;
+            if (s + 1 + nb > se) return false;
+            if (nb) {
+                v = 0;
+                for (uint32_t q = 0; q < nb; q++) v |= (uint32_t)ld8(s + 1 + q) << (8 * q);
+            }
+            s += 1 + nb;
+            length = (uint64_t)v + 1;
+            if (length > dlen - d || length > se - s) return false;
+            d += length;
+            s += length;
+            continue;
+        }
+        const uint32_t nb = (tag & 3) == 1 ? 1u : (tag & 3) == 2 ? 2u : 4u;
+        if (s + 1 + nb > se) return false;
+        if ((tag & 3) == 1) {
+            length = 4 + ((tag >> 2) & 7);
+            offset = ((tag & 0xe0u) << 3) | ld8(s + 1);
+        } else {
+            length = 1 + (tag >> 2);
+            for (uint32_t q = 0; q < nb; q++) offset |= (uint64_t)ld8(s + 1 + q) << (8 * q);
+        }
+        s += 1 + nb;
+        if (offset == 0 || d < offset || length > dlen - d) return false;
+        d += length;
+    }
+    return d == dlen;
+}
+
+// Writer.Get's read of the record it found (writer.go:190-228): ReadAt inside the file,
+// readRecord non-nil (block2.go:57-66), compressor.Decode without error and with a non-nil value
+// (snappy.Decode of a 0-length stream returns a nil slice).  Any failure makes Bithash.Get fall
+// through to GetFileNumMap -> Reader.Get (bithash.go:102-107).
+__device__ bool writer_record_ok(uint64_t base, uint64_t src_len, const bhg_handle &h, int codec) {
+    if (h.offset > src_len || (uint64_t)h.length > src_len - h.offset || h.length < 12) return false;
+    const uint64_t p = base + h.offset, end = base + src_len;
+    const uint32_t k = ldu32(p, end), v = ldu32(p + 4, end);
+    if (k == 0 || v == 0 || (uint64_t)12 + k + v != (uint64_t)h.length) return false;
+    if (codec != BHG_CODEC_SNAPPY) return true;  // noCompressor.Decode returns the non-empty value
+    uint64_t dlen = 0;
+    return snappy_stream_ok(p + 12 + k, v, dlen) && dlen != 0;
+}
+
+// Bithash.Get (bithash.go:101-119): the open writer of file_num first (Writer.Get, final only
+// when it returns a value without error), then GetFileNumMap(fn) (:264-273; 0 ->
+// ErrBhFileNumZero) and Reader.Get on that table
 template <bool HAVE_HASH>
 __global__ __launch_bounds__(256) void k_bithash_get(const uint8_t *__restrict__ src, uint64_t src_len,
                                                      const bhg_writer_index *__restrict__ writers, uint32_t nwriters,
@@ -282,7 +353,7 @@ __global__ __launch_bounds__(256) void k_bithash_get(const uint8_t *__restrict__
                                                      const uint32_t *__restrict__ fn_table, uint32_t fn_count,
                                                      const uint8_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
                                                      const uint32_t *__restrict__ file_nums,
-                                                     const uint32_t *__restrict__ khash, uint32_t n,
+                                                     const uint32_t *__restrict__ khash, int codec, uint32_t n,
                                                      bhg_handle *__restrict__ out_h, uint32_t *__restrict__ out_st) {
     const uint64_t base = (uint64_t)src, end = base + src_len;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -297,8 +368,9 @@ __global__ __launch_bounds__(256) void k_bithash_get(const uint8_t *__restrict__
         for (uint32_t w = 0; w < nwriters && !done; w++) {
             const bhg_writer_index W = writers[w];
             if (W.file_num == fn) {
-                done = writer_lookup(base, end, W, kp, klen, kh, h);
+                done = writer_lookup(base, end, W, kp, klen, kh, h) && writer_record_ok(base, src_len, h, codec);
                 if (done) st = BHG_ST_OK;
+                else h = bhg_handle{0, 0, 0};
                 break;
             }
         }
@@ -349,18 +421,20 @@ hipError_t launch_get(const Launch &L, const uint8_t *src, uint64_t src_len, con
 hipError_t launch_bithash_get(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
                               uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
                               const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
-                              const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_h,
-                              uint32_t *out_st) {
+                              const uint32_t *file_nums, const uint32_t *khash, int codec, uint32_t n,
+                              bhg_handle *out_h, uint32_t *out_st) {
     uint64_t need = (n + 255) / 256;
     uint64_t cap = (uint64_t)L.num_cus * 16;
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
     if (khash)
         hipLaunchKernelGGL(k_bithash_get<true>, dim3(grid), dim3(256), 0, L.stream, src, src_len, writers, nwriters,
-                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, n, out_h, out_st);
+                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, codec, n, out_h,
+                           out_st);
     else
         hipLaunchKernelGGL(k_bithash_get<false>, dim3(grid), dim3(256), 0, L.stream, src, src_len, writers, nwriters,
-                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, n, out_h, out_st);
+                           tables, ntables, fn_map, fn_table, fn_count, keys, key_off, file_nums, khash, codec, n, out_h,
+                           out_st);
     return hipGetLastError();
 }
 

@@ -84,8 +84,8 @@ hipError_t launch_get(const Launch &L, const uint8_t *src, uint64_t src_len, con
 hipError_t launch_bithash_get(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
                               uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
                               const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
-                              const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_h,
-                              uint32_t *out_st);
+                              const uint32_t *file_nums, const uint32_t *khash, int codec, uint32_t n,
+                              bhg_handle *out_h, uint32_t *out_st);
 size_t writer_index_scratch_bytes(uint32_t n);
 hipError_t launch_writer_index(const Launch &L, const uint32_t *khash, uint32_t n, uint32_t *sorted,
                                uint32_t *sorted_kh, void *scratch);

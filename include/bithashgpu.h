@@ -396,7 +396,10 @@ int bhg_writer_index_build(bhg_ctx *ctx, const uint32_t *khash, uint32_t n, uint
 
 /* Bithash.Get (bithash.go:101-119) for n queries (UserKey keys[key_off[i] : key_off[i+1]],
  * khash[i] or hash.Fnv32 of the key when khash is null, fileNum file_nums[i]):
- *   1. the open writer with that fileNum (writers[], nwriters): Writer.Get -> OK on a hit;
+ *   1. the open writer with that fileNum (writers[], nwriters): Writer.Get -> OK on a hit whose
+ *      read succeeds (writer.go:190-228: the record inside src, readRecord non-nil, and with
+ *      codec BHG_CODEC_SNAPPY a snappy stream that decodes without error to >= 1 byte); any
+ *      other writer outcome falls through to 2, as Go's `err == nil && value != nil` test does;
  *   2. dst = fn_map[fn] (GetFileNumMap, :264-273; fn >= fn_count or 0 -> BHG_ST_FILE_NUM_ZERO);
  *   3. the opened table tables[fn_table[dst]] (bhtReaders; none -> BHG_ST_NOT_FOUND): Reader.Get's
  *      index path as bhg_get_batch (OK / NOT_FOUND / ILLEGAL_LENGTH).
@@ -405,8 +408,8 @@ int bhg_writer_index_build(bhg_ctx *ctx, const uint32_t *khash, uint32_t n, uint
 int bhg_bithash_get_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_writer_index *writers,
                           uint32_t nwriters, const bhg_table *tables, uint32_t ntables, const uint32_t *fn_map,
                           const uint32_t *fn_table, uint32_t fn_count, const uint8_t *keys, const uint64_t *key_off,
-                          const uint32_t *file_nums, const uint32_t *khash, uint32_t n, bhg_handle *out_handles,
-                          uint32_t *out_status, void *stream);
+                          const uint32_t *file_nums, const uint32_t *khash, int codec, uint32_t n,
+                          bhg_handle *out_handles, uint32_t *out_status, void *stream);
 
 #ifdef __cplusplus
 }

@@ -422,12 +422,20 @@ def bithash_get_handle(writers, files, fn_map, ukey, fn, khash=None):
     """Bithash.Get (bithash.go:101-119) without the read: writers = {fileNum: open Writer}
     (rwwWriters), files = {fileNum: closed table bytes} (bhtReaders), fn_map = GetFileNumMap's map.
     Returns (status, fileNum, (off, len)) with status "OK", "NOT_FOUND", "ILLEGAL_LENGTH" or
-    "FILE_NUM_ZERO"; a writer hit is final (its records are well formed)."""
+    "FILE_NUM_ZERO".  A writer hit is final only when Writer.Get returns err == nil and a
+    non-nil value (bithash.go:102-107): its read (writer.go:190-228) can fail on the record
+    (ErrBhReadRecordNil, ErrBhReadAtIncomplete) or the snappy stream, and snappy.Decode of a
+    0-length stream returns a nil slice; each of those falls through to GetFileNumMap."""
     w = writers.get(fn)
     if w is not None:
         bh = writer_get_handle(w, ukey, khash)
         if bh is not None:
-            return "OK", fn, bh
+            try:
+                val = _read_data(bytes(w.file), bh, w.compressor)
+            except (BithashError, O.SnappyCorrupt):
+                val = None
+            if val is not None and (w.compressor != 1 or len(val) > 0):
+                return "OK", fn, bh
     dst = fn_map.get(fn, 0)
     if dst == 0:
         return "FILE_NUM_ZERO", 0, (0, 0)

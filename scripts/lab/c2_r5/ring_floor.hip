@@ -1,0 +1,206 @@
+// ring_floor.hip -- LAB (not product code): the loader-only floor of an LDS-DMA ring
+// (VERDICT r4 #1 gate).  One 64*(1+NC)-thread workgroup per CU streams a contiguous
+// 1/grid share of a 1.076 GB buffer HBM -> LDS with global_load_lds_dwordx4 (1 KiB contiguous
+// per wave instruction) from ONE dedicated loader wave into a ring of NS slots of NI KiB.
+// Per slot a FULL word (loader -> consumers) and a FREE word (consumers -> loader) in LDS;
+// the loader keeps D slots in flight behind a compile-time s_waitcnt vmcnt(NI*(D-1)).
+// Consumer waves take slots round-robin and release them (READ=1: after reading every byte
+// of the slot with ds_read_b128; READ=0: at once).  STORE=1 adds the C2 descriptor stores
+// (40 B per 1,076 B of stream, non-temporal) from the consumers.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+#define STR2(x) #x
+#define STR(x) STR2(x)
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+template <int NT>
+__device__ __forceinline__ void glds16(uint64_t gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    if (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_poll(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return uni(v);
+}
+__device__ __forceinline__ void lds_put(uint32_t a, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 lds_ld128(uint32_t a) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>((size_t)a);
+}
+
+template <int NI, int NS, int D, int NT, int NC, int READ, int STORE>
+__global__ __launch_bounds__(64 * (1 + NC)) void k_floor(const uint8_t *__restrict__ src, uint64_t len,
+                                                        uint64_t *__restrict__ out, uint32_t *__restrict__ sink) {
+    constexpr uint32_t SB = NI * 1024;
+    static_assert(NI * (D - 1) <= 63, "vmcnt field");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(NS * SB) / 4 + 2 * NS];
+    const uint32_t rb = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)lds;
+    const uint32_t fullw = rb + NS * SB, freew = fullw + 4 * NS;
+    const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+    if (threadIdx.x < 2 * NS) lds[(NS * SB) / 4 + threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t part = ((len / 16) / gridDim.x) * 16;
+    const uint64_t lo = (uint64_t)src + blockIdx.x * part;
+    const uint64_t hi = blockIdx.x + 1 == gridDim.x ? (uint64_t)src + len : lo + part;
+    const uint32_t ntile = (uint32_t)((hi - lo + SB - 1) / SB);
+    if (wv == 0) {  // ---- loader
+        for (uint32_t t = 0; t < ntile; t++) {
+            const uint32_t s = t % NS;
+            if (t >= NS) {
+                uint32_t spin = 0;  // bounded: a protocol bug must not hang the GPU
+                while (lds_poll(freew + 4 * s) < t - NS + 1 && ++spin < (1u << 20)) __builtin_amdgcn_s_sleep(1);
+                if (spin >= (1u << 20)) sink[1] = 1;
+            }
+            const uint64_t tb = lo + (uint64_t)t * SB;
+#pragma unroll
+            for (uint32_t k = 0; k < NI; k++) {
+                uint64_t a = tb + 1024ull * k + 16ull * lane;
+                const bool act = a + 16 <= hi || lane == 0;
+                if (a + 16 > hi) a = hi - 16;
+                if (act) glds16<NT>(a, uni(rb + s * SB + 1024 * k));
+            }
+            if (t >= D - 1) {
+                wait_vm<NI * (D - 1)>();
+                const uint32_t tp = t - (D - 1);
+                lds_put(fullw + 4 * (tp % NS), tp + 1);
+            }
+        }
+        wait_vm<0>();
+        for (uint32_t tp = ntile >= D - 1 ? ntile - (D - 1) : 0u; tp < ntile; tp++) lds_put(fullw + 4 * (tp % NS), tp + 1);
+    } else {  // ---- consumers
+        const uint32_t c = wv - 1;
+        u32x4 acc = {0, 0, 0, 0};
+        for (uint32_t t = c; t < ntile; t += NC) {
+            const uint32_t s = t % NS;
+            uint32_t spin = 0;
+            while (lds_poll(fullw + 4 * s) < t + 1 && ++spin < (1u << 20)) __builtin_amdgcn_s_sleep(1);
+            if (spin >= (1u << 20)) sink[1] = 1;
+            if (READ) {
+#pragma unroll
+                for (uint32_t k = 0; k < NI; k++) acc ^= lds_ld128(rb + s * SB + 1024 * k + 16 * lane);
+            }
+            lds_put(freew + 4 * s, t + 1);
+            if (STORE) {  // 40 B per 1,076 B: ~15.2 descriptors per 16 KiB, lanes 0..(5*SB/1076) write 8 B
+                const uint32_t nd = (SB * 5) / 1076;  // 8-B words of descriptors for this slot
+                const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * nd;
+                if (lane < nd) __builtin_nontemporal_store((uint64_t)(acc.x + lane), out + d0 + lane);
+            }
+        }
+        if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = lane;
+    }
+}
+
+// register-staged reference sweep: every wave of 8 per CU streams 16 B per lane, 4 loads in flight
+__global__ __launch_bounds__(512) void k_sweep(const uint8_t *__restrict__ src, uint64_t len, uint32_t *sink) {
+    const uint64_t nq = len / 16;
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(src);
+    u32x4 acc = {0, 0, 0, 0};
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < nq; i += 4 * stride) {
+        const u32x4 a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(p + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(p + i + 2 * stride), d = __builtin_nontemporal_load(p + i + 3 * stride);
+        acc ^= a ^ b ^ c ^ d;
+    }
+    for (; i < nq; i += stride) acc ^= p[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;
+}
+
+typedef void (*lfn)(const uint8_t *, uint64_t, uint64_t *, uint32_t *, int, hipStream_t);
+template <int NI, int NS, int D, int NT, int NC, int READ, int STORE>
+static void launch(const uint8_t *src, uint64_t len, uint64_t *out, uint32_t *sink, int cus, hipStream_t s) {
+    hipLaunchKernelGGL((k_floor<NI, NS, D, NT, NC, READ, STORE>), dim3(cus), dim3(64 * (1 + NC)), 0, s, src, len, out, sink);
+}
+static void launch_sweep(const uint8_t *src, uint64_t len, uint64_t *, uint32_t *sink, int cus, hipStream_t s) {
+    hipLaunchKernelGGL(k_sweep, dim3(cus * 4), dim3(512), 0, s, src, len, sink);
+}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 30;
+    const uint64_t len = 1076ull * 1000000ull;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    uint8_t *src;
+    uint64_t *out;
+    uint32_t *sink;
+    CK(hipMalloc(&src, len + 4096));
+    CK(hipMalloc(&out, 64ull << 20));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(src, 0x5a, len + 4096));
+    CK(hipMemset(sink, 0, 64));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    struct V { const char *name; lfn fn; };
+    const V vs[] = {
+        {"sweep_reg", launch_sweep},
+        {"ni16_ns6_d4_nt", launch<16, 6, 4, 1, 7, 0, 0>},
+        {"ni16_ns6_d4_def", launch<16, 6, 4, 0, 7, 0, 0>},
+        {"ni16_ns6_d4_nt_read", launch<16, 6, 4, 1, 7, 1, 0>},
+        {"ni16_ns6_d4_nt_rd_st", launch<16, 6, 4, 1, 7, 1, 1>},
+        {"ni8_ns12_d7_nt", launch<8, 12, 7, 1, 7, 0, 0>},
+        {"ni8_ns12_d5_nt", launch<8, 12, 5, 1, 7, 0, 0>},
+        {"ni8_ns12_d7_nt_rd_st", launch<8, 12, 7, 1, 7, 1, 1>},
+        {"ni9_ns10_d5_nt", launch<9, 10, 5, 1, 7, 0, 0>},
+        {"ni9_ns11_d6_nt_rd_st", launch<9, 11, 6, 1, 7, 1, 1>},
+        {"ni4_ns24_d15_nt", launch<4, 24, 15, 1, 7, 0, 0>},
+        {"ni16_ns8_d4_nt_3c", launch<16, 8, 4, 1, 3, 0, 0>},
+        {"sweep_reg_b", launch_sweep},
+    };
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int it = 0; it < 100; it++) launch_sweep(src, len, out, sink, cus, s);  // clocks
+    CK(hipStreamSynchronize(s));
+    for (const V &v : vs) {
+        v.fn(src, len, out, sink, cus, s);
+        CK(hipStreamSynchronize(s));
+        CK(hipGetLastError());
+        std::vector<float> ts;
+        for (int it = 0; it < iters; it++) {
+            CK(hipEventRecord(a, s));
+            v.fn(src, len, out, sink, cus, s);
+            CK(hipEventRecord(b, s));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const float med = ts[ts.size() / 2];
+        uint32_t hs[2];
+        CK(hipMemcpy(hs, sink, 8, hipMemcpyDeviceToHost));
+        if (hs[1]) { printf("%s: POLL TIMEOUT\n", v.name); return 1; }
+        printf("%-24s median %.4f ms best %.4f  %.2f TB/s (1.076 GB)  C2-frac-if-kernel %.4f\n", v.name, med, ts[0],
+               len / (med * 1e-3) / 1e12, 1136e6 / (med * 1e-3) / 8e12);
+        fflush(stdout);
+    }
+    return 0;
+}

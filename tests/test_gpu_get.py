@@ -246,3 +246,85 @@ def test_bithash_get_open_writer_and_filenum_map(codec):
 def struct_len(buf, off):
     import struct
     return struct.unpack_from("<I", buf, off + 4)[0]
+
+
+@pytest.mark.parametrize("compressor", [0, 1])
+def test_bithash_get_writer_read_failure_falls_through(codec, compressor):
+    """Bithash.Get keeps an open writer's answer only when Writer.Get returns a value without
+    error (bithash.go:102-107).  Open-writer records that read as nil -- an empty value
+    (NoCompressor: readRecord nil, ErrBhReadRecordNil; snappy: a 0-length stream decodes to a nil
+    slice), a corrupted valueSize, a corrupted snappy stream -- fall through GetFileNumMap to the
+    closed table (hit or ErrBhNotFound); a later good add of the same key is final again.
+    Checked against the restated Bithash.Get (oracle/table.py bithash_get_handle)."""
+    import struct
+    from bitalosdb_amd._lib import ST_FILE_NUM_ZERO, WRITER_INDEX_DT
+    from bitalosdb_amd.codec import handles_tensor
+    rng = random.Random(1000 + compressor)
+    f5, w5 = _writer_table(rng, 300, 5)
+    files = {5: f5}
+    src, tabs = _concat([f5])
+    uniq5 = list(dict.fromkeys(w5))
+    rng.shuffle(uniq5)
+    good, empty, corrupt, healed = uniq5[:30], uniq5[30:60], uniq5[60:80], uniq5[80:100]
+    fresh_empty = [b"fe%03d" % i for i in range(10)]
+    fresh_good = [b"fg%03d" % i for i in range(10)]
+    w = T.Writer(9, 1 << 30, compressor=compressor)
+
+    def val():
+        return bytes(rng.randrange(65, 91) for _ in range(rng.randrange(10, 100)))
+    adds = [(k, val()) for k in good + corrupt + fresh_good] + [(k, b"") for k in empty + fresh_empty + healed]
+    rng.shuffle(adds)
+    adds += [(k, val()) for k in healed]              # the last add of a healed key is good
+    recs, corrupt_at = [], {}
+    for i, (k, v) in enumerate(adds):
+        off = w.current_offset
+        w.add(k, ((i + 1) << 8) | 1, v)
+        recs.append((off, w.current_offset - off))
+        if k in corrupt:
+            corrupt_at[k] = off
+    for k, off in corrupt_at.items():                 # after the adds: the index keeps the handles
+        kl, vl = struct.unpack_from("<II", w.file, off)
+        if compressor == 0:
+            struct.pack_into("<I", w.file, off + 4, vl + 1)            # 12 + k + v != len(buf)
+        else:
+            assert w.file[off + 12 + kl] < 127
+            w.file[off + 12 + kl] += 1                                 # decodedLen one past the body
+    wbase = len(src) + 3
+    src = src + bytes(3) + bytes(w.file)
+    rec_h = np.array([(wbase + o, ln, 0) for o, ln in recs], dtype=O.HANDLE_DT)
+    dev = codec.device
+    with torch.cuda.stream(codec.stream):
+        src_t = torch.from_numpy(np.frombuffer(src, np.uint8).copy()).to(dev)
+        rec_t = handles_tensor(rec_h, dev)
+        kh_t = torch.from_numpy(np.array([O.fnv32(k) for k, _ in adds], dtype=np.uint32).view(np.int32)).to(dev)
+        srt, skh = codec.writer_index(kh_t, len(adds))
+    writers = np.zeros(1, dtype=WRITER_INDEX_DT)
+    writers[0] = (rec_t.data_ptr(), srt.data_ptr(), skh.data_ptr(), len(adds), 9)
+    fn_map_d = {5: 5, 9: 5}
+    fn_count = 12
+    fn_map = np.zeros(fn_count, np.uint32)
+    for s_, d_ in fn_map_d.items():
+        fn_map[s_] = d_
+    fn_table = np.full(fn_count, 0xFFFFFFFF, np.uint32)
+    fn_table[5] = 0
+    missing = [b"zz%03d" % i for i in range(10)]
+    qs = [(9, k) for k in good + empty + corrupt + healed + fresh_empty + fresh_good + missing]
+    qs += [(5, k) for k in good[:10]] + [(10, k) for k in empty[:5]]
+    h_t, s_t = codec.bithash_get(src_t, writers, tabs, fn_map, fn_table, [q[1] for q in qs], [q[0] for q in qs],
+                                 compressor=compressor)
+    codec.sync()
+    h = h_t.cpu().numpy().view(np.uint8).view(O.HANDLE_DT)
+    st = s_t.cpu().numpy().view(np.uint32)
+    code = dict(ST, FILE_NUM_ZERO=ST_FILE_NUM_ZERO)
+    base_of = {5: int(tabs["base"][0]), 9: wbase}
+    fell = hit = 0
+    for i, (fn, k) in enumerate(qs):
+        es, efn, (eo, el) = T.bithash_get_handle({9: w}, files, fn_map_d, k, fn)
+        assert st[i] == code[es], (i, fn, k, es, st[i])
+        if es == "OK":
+            assert int(h["offset"][i]) == base_of[efn] + eo and int(h["length"][i]) == el, (i, fn, k)
+            if fn == 9:
+                fell += efn == 5
+                hit += efn == 9
+    # every failure class fell through to table 5, every good writer record answered itself
+    assert fell == len(empty) + len(corrupt) and hit == len(good) + len(healed) + len(fresh_good)
