@@ -38,6 +38,26 @@ __device__ __forceinline__ void glds16(uint64_t gsrc, uint32_t lds_dst) {
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
+// four 1-KiB pieces from one address register and one M0: the instruction offset field moves
+// both the global and the LDS address (llvm.amdgcn.global.load.lds semantics)
+template <int NT>
+__device__ __forceinline__ void glds16x4(uint64_t gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    if (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off nt\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:1024 nt\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:2048 nt\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:3072 nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:3072\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -55,8 +75,8 @@ __device__ __forceinline__ u32x4 lds_ld128(uint32_t a) {
     return *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>((size_t)a);
 }
 
-template <int NI, int NS, int D, int NT, int NC, int READ, int STORE>
-__global__ __launch_bounds__(64 * (1 + NC)) void k_floor(const uint8_t *__restrict__ src, uint64_t len,
+template <int NI, int NS, int D, int NT, int NC, int READ, int STORE, int LD = 1, int FAST = 0>
+__global__ __launch_bounds__(64 * (LD + NC)) void k_floor(const uint8_t *__restrict__ src, uint64_t len,
                                                         uint64_t *__restrict__ out, uint32_t *__restrict__ sink) {
     constexpr uint32_t SB = NI * 1024;
     static_assert(NI * (D - 1) <= 63, "vmcnt field");
@@ -70,8 +90,9 @@ __global__ __launch_bounds__(64 * (1 + NC)) void k_floor(const uint8_t *__restri
     const uint64_t lo = (uint64_t)src + blockIdx.x * part;
     const uint64_t hi = blockIdx.x + 1 == gridDim.x ? (uint64_t)src + len : lo + part;
     const uint32_t ntile = (uint32_t)((hi - lo + SB - 1) / SB);
-    if (wv == 0) {  // ---- loader
-        for (uint32_t t = 0; t < ntile; t++) {
+    if (wv < LD) {  // ---- loader(s): loader l takes tiles l, l + LD, ...
+        uint32_t tl = 0;  // this loader's tile count
+        for (uint32_t t = wv; t < ntile; t += LD, tl++) {
             const uint32_t s = t % NS;
             if (t >= NS) {
                 uint32_t spin = 0;  // bounded: a protocol bug must not hang the GPU
@@ -79,41 +100,104 @@ __global__ __launch_bounds__(64 * (1 + NC)) void k_floor(const uint8_t *__restri
                 if (spin >= (1u << 20)) sink[1] = 1;
             }
             const uint64_t tb = lo + (uint64_t)t * SB;
+            if (FAST && tb + SB <= hi) {
+                static_assert(!FAST || NI % 4 == 0, "x4 batches");
 #pragma unroll
-            for (uint32_t k = 0; k < NI; k++) {
-                uint64_t a = tb + 1024ull * k + 16ull * lane;
-                const bool act = a + 16 <= hi || lane == 0;
-                if (a + 16 > hi) a = hi - 16;
-                if (act) glds16<NT>(a, uni(rb + s * SB + 1024 * k));
+                for (uint32_t k = 0; k < NI; k += 4) glds16x4<NT>(tb + 1024ull * k + 16ull * lane, uni(rb + s * SB + 1024 * k));
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < NI; k++) {
+                    uint64_t a = tb + 1024ull * k + 16ull * lane;
+                    const bool act = a + 16 <= hi || lane == 0;
+                    if (a + 16 > hi) a = hi - 16;
+                    if (act) glds16<NT>(a, uni(rb + s * SB + 1024 * k));
+                }
             }
-            if (t >= D - 1) {
+            if (tl >= D - 1) {
                 wait_vm<NI * (D - 1)>();
-                const uint32_t tp = t - (D - 1);
+                const uint32_t tp = t - (D - 1) * LD;
                 lds_put(fullw + 4 * (tp % NS), tp + 1);
+                if (STORE == 10) {
+                    const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + tp) * 80;
+                    const u32x4 v = {lane, 1, 2, 3};
+                    if (lane < 40) reinterpret_cast<u32x4 *>(out + d0)[lane] = v;
+                }
             }
         }
         wait_vm<0>();
-        for (uint32_t tp = ntile >= D - 1 ? ntile - (D - 1) : 0u; tp < ntile; tp++) lds_put(fullw + 4 * (tp % NS), tp + 1);
+        // publish this loader's last D-1 tiles
+        for (uint32_t q = tl >= D - 1 ? tl - (D - 1) : 0u; q < tl; q++) {
+            const uint32_t tp = wv + q * LD;
+            lds_put(fullw + 4 * (tp % NS), tp + 1);
+        }
     } else {  // ---- consumers
-        const uint32_t c = wv - 1;
+        const uint32_t c = wv - LD;
+        uint32_t bad = 0;
         u32x4 acc = {0, 0, 0, 0};
         for (uint32_t t = c; t < ntile; t += NC) {
             const uint32_t s = t % NS;
             uint32_t spin = 0;
             while (lds_poll(fullw + 4 * s) < t + 1 && ++spin < (1u << 20)) __builtin_amdgcn_s_sleep(1);
             if (spin >= (1u << 20)) sink[1] = 1;
-            if (READ) {
+            if (READ == 1) {
 #pragma unroll
                 for (uint32_t k = 0; k < NI; k++) acc ^= lds_ld128(rb + s * SB + 1024 * k + 16 * lane);
+            } else if (READ == 2) {  // verify: word w of the buffer holds w (host fill)
+                const uint64_t tb = lo + (uint64_t)t * SB;
+#pragma unroll
+                for (uint32_t k = 0; k < NI; k++) {
+                    const uint64_t a = tb + 1024ull * k + 16ull * lane;
+                    if (a + 16 <= hi) {
+                        const u32x4 v = lds_ld128(rb + s * SB + 1024 * k + 16 * lane);
+                        const uint32_t w0 = (uint32_t)((a - (uint64_t)src) >> 2);
+                        bad += (v.x != w0) + (v.y != w0 + 1) + (v.z != w0 + 2) + (v.w != w0 + 3);
+                    }
+                }
             }
             lds_put(freew + 4 * s, t + 1);
-            if (STORE) {  // 40 B per 1,076 B: ~15.2 descriptors per 16 KiB, lanes 0..(5*SB/1076) write 8 B
+            if (STORE == 1) {  // 40 B per 1,076 B: ~15.2 descriptors per 16 KiB, lanes 0..(5*SB/1076) write 8 B
                 const uint32_t nd = (SB * 5) / 1076;  // 8-B words of descriptors for this slot
                 const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * nd;
                 if (lane < nd) __builtin_nontemporal_store((uint64_t)(acc.x + lane), out + d0 + lane);
+            } else if (STORE == 2 || STORE == 3) {  // 16 B per lane, the slot's 40 B x 15.2 records contiguous
+                const uint32_t nq = (SB * 40 / 1076 + 15) / 16;
+                const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * (nq * 2);
+                const u32x4 v = {acc.x + lane, acc.y, acc.z, acc.w};
+                if (lane < nq) {
+                    if (STORE == 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(out + d0) + lane);
+                    else reinterpret_cast<u32x4 *>(out + d0)[lane] = v;
+                }
+            } else if (STORE == 4) {  // 8 B per lane, plain
+                const uint32_t nd = (SB * 5) / 1076;
+                const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * nd;
+                if (lane < nd) out[d0 + lane] = (uint64_t)(acc.x + lane);
+            } else if (STORE == 6) {  // 16 B per lane, plain, into a 4 KiB region per CU (L2 resident)
+                const uint32_t nq = (SB * 40 / 1076 + 15) / 16;
+                const uint64_t d0 = (uint64_t)blockIdx.x * 512 + (t & 3) * 80;
+                const u32x4 v = {acc.x + lane, acc.y, acc.z, acc.w};
+                if (lane < nq) reinterpret_cast<u32x4 *>(out + d0)[lane] = v;
+            } else if (STORE == 8) {  // 16 B per lane, plain, line-aligned 640-B chunks
+                const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * 80;
+                const u32x4 v = {acc.x + lane, acc.y, acc.z, acc.w};
+                if (lane < 40) reinterpret_cast<u32x4 *>(out + d0)[lane] = v;
+            } else if (STORE == 9) {  // batched: every 8th tile of this consumer, 8 x 640 B, plain
+                if (((t / NC) & 7) == 7) {
+                    const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * 80;
+                    const u32x4 v = {acc.x + lane, acc.y, acc.z, acc.w};
+                    for (uint32_t q = lane; q < 8 * 40; q += 64) reinterpret_cast<u32x4 *>(out + d0)[q] = v;
+                }
+            } else if (STORE == 5) {  // batched: every 4th tile of this consumer, 4 tiles' descriptors, 16 B per lane
+                const uint32_t nq = (SB * 40 / 1076 + 15) / 16;
+                if (((t / NC) & 3) == 3) {
+                    const uint64_t d0 = ((uint64_t)blockIdx.x * ntile + t) * (nq * 2);
+                    const u32x4 v = {acc.x + lane, acc.y, acc.z, acc.w};
+                    for (uint32_t q = lane; q < 4 * nq; q += 64)
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(out + d0) + q);
+                }
             }
         }
         if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = lane;
+        if (READ == 2 && bad) atomicAdd(sink + 2, bad);
     }
 }
 
@@ -134,9 +218,14 @@ __global__ __launch_bounds__(512) void k_sweep(const uint8_t *__restrict__ src, 
 }
 
 typedef void (*lfn)(const uint8_t *, uint64_t, uint64_t *, uint32_t *, int, hipStream_t);
-template <int NI, int NS, int D, int NT, int NC, int READ, int STORE>
+template <int NI, int NS, int D, int NT, int NC, int READ, int STORE, int LD = 1, int FAST = 0>
 static void launch(const uint8_t *src, uint64_t len, uint64_t *out, uint32_t *sink, int cus, hipStream_t s) {
-    hipLaunchKernelGGL((k_floor<NI, NS, D, NT, NC, READ, STORE>), dim3(cus), dim3(64 * (1 + NC)), 0, s, src, len, out, sink);
+    hipLaunchKernelGGL((k_floor<NI, NS, D, NT, NC, READ, STORE, LD, FAST>), dim3(cus), dim3(64 * (LD + NC)), 0, s, src,
+                       len, out, sink);
+}
+__global__ void k_iota(uint32_t *p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = (uint32_t)i;
 }
 static void launch_sweep(const uint8_t *src, uint64_t len, uint64_t *, uint32_t *sink, int cus, hipStream_t s) {
     hipLaunchKernelGGL(k_sweep, dim3(cus * 4), dim3(512), 0, s, src, len, sink);
@@ -154,25 +243,25 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&src, len + 4096));
     CK(hipMalloc(&out, 64ull << 20));
     CK(hipMalloc(&sink, 64));
-    CK(hipMemset(src, 0x5a, len + 4096));
+    hipLaunchKernelGGL(k_iota, dim3(4096), dim3(256), 0, 0, (uint32_t *)src, (len + 4096) / 4);
+    CK(hipDeviceSynchronize());
     CK(hipMemset(sink, 0, 64));
     hipStream_t s;
     CK(hipStreamCreate(&s));
     struct V { const char *name; lfn fn; };
     const V vs[] = {
         {"sweep_reg", launch_sweep},
-        {"ni16_ns6_d4_nt", launch<16, 6, 4, 1, 7, 0, 0>},
-        {"ni16_ns6_d4_def", launch<16, 6, 4, 0, 7, 0, 0>},
-        {"ni16_ns6_d4_nt_read", launch<16, 6, 4, 1, 7, 1, 0>},
-        {"ni16_ns6_d4_nt_rd_st", launch<16, 6, 4, 1, 7, 1, 1>},
-        {"ni8_ns12_d7_nt", launch<8, 12, 7, 1, 7, 0, 0>},
-        {"ni8_ns12_d5_nt", launch<8, 12, 5, 1, 7, 0, 0>},
-        {"ni8_ns12_d7_nt_rd_st", launch<8, 12, 7, 1, 7, 1, 1>},
-        {"ni9_ns10_d5_nt", launch<9, 10, 5, 1, 7, 0, 0>},
-        {"ni9_ns11_d6_nt_rd_st", launch<9, 11, 6, 1, 7, 1, 1>},
-        {"ni4_ns24_d15_nt", launch<4, 24, 15, 1, 7, 0, 0>},
-        {"ni16_ns8_d4_nt_3c", launch<16, 8, 4, 1, 3, 0, 0>},
-        {"sweep_reg_b", launch_sweep},
+        {"fast_ni16_d4", launch<16, 6, 4, 1, 7, 0, 0, 1, 1>},
+        {"st3_16B_plain", launch<16, 6, 4, 1, 7, 0, 3, 1, 1>},
+        {"st6_L2_resident", launch<16, 6, 4, 1, 7, 0, 6, 1, 1>},
+        {"st8_aligned640", launch<16, 6, 4, 1, 7, 0, 8, 1, 1>},
+        {"st9_batch8_aligned", launch<16, 6, 4, 1, 7, 0, 9, 1, 1>},
+        {"st10_loader_stores", launch<16, 6, 4, 1, 7, 0, 10, 1, 1>},
+        {"st8_def_loads", launch<16, 6, 4, 0, 7, 0, 8, 1, 1>},
+        {"st8_ns8_d3", launch<16, 8, 3, 1, 7, 0, 8, 1, 1>},
+        {"st8_2ld", launch<16, 8, 3, 1, 6, 0, 8, 2, 1>},
+        {"st3_again", launch<16, 6, 4, 1, 7, 0, 3, 1, 1>},
+        {"fast_ni16_d4_again", launch<16, 6, 4, 1, 7, 0, 0, 1, 1>},
     };
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -195,9 +284,10 @@ int main(int argc, char **argv) {
         }
         std::sort(ts.begin(), ts.end());
         const float med = ts[ts.size() / 2];
-        uint32_t hs[2];
-        CK(hipMemcpy(hs, sink, 8, hipMemcpyDeviceToHost));
+        uint32_t hs[3];
+        CK(hipMemcpy(hs, sink, 12, hipMemcpyDeviceToHost));
         if (hs[1]) { printf("%s: POLL TIMEOUT\n", v.name); return 1; }
+        if (hs[2]) { printf("%s: VERIFY MISMATCH words %u\n", v.name, hs[2]); CK(hipMemset(sink, 0, 64)); }
         printf("%-24s median %.4f ms best %.4f  %.2f TB/s (1.076 GB)  C2-frac-if-kernel %.4f\n", v.name, med, ts[0],
                len / (med * 1e-3) / 1e12, 1136e6 / (med * 1e-3) / 8e12);
         fflush(stdout);
