@@ -615,12 +615,17 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
             return BHG_ENOMEM;
         }
     }
-    struct PoolWait {  // no return leaves a host copy running into the caller's buffers
+    // No return, error paths included, leaves a copy kernel, a D2H copy or a host copy running into
+    // the caller's buffers: both streams are drained (best effort), then the host copy threads.
+    struct PoolWait {
         HostCopyPool *p;
+        hipStream_t s1, s2;
         ~PoolWait() {
+            (void)hipStreamSynchronize(s1);
+            (void)hipStreamSynchronize(s2);
             if (p) p->wait();
         }
-    } pool_wait{staged ? c->hpool : nullptr};
+    } pool_wait{staged ? c->hpool : nullptr, sc, sd};
     bool dpend[bhg_ctx::kPipe] = {false, false, false};  // the slot's last D2H has an event to wait for
     uint64_t vbase = 0;                                   // the batch offset of the next chunk's first value
     uint64_t prev_off = 0;

@@ -202,14 +202,15 @@ inline void build_xtab(uint32_t *out) {
     for (uint32_t j = 0; j < kXLongN; j++) crc32c_shift_table(1ull << (10 + j), out + kXLong + 1024 * j);
 }
 
-// Shift tables of the LDS-DMA ring decode (bhg_decode_ring.hip), in this order: Z_68 (fold of a
-// window's two 68-B chains), then Z_{136 * 2^k}, k = 0..6 (136 .. 8,704 B): a lane's distance to
-// the record end (k = 0..2), the Horner step over 8 windows (Z_1088, k = 3), the head's shift past
-// m - 1 windows (by the bits of m - 1) and the big-record path's 64-lane steps (Z_8704).
-constexpr uint32_t kRingZN = 8;
+// Shift tables of the LDS-DMA ring decode (bhg_decode_ring.hip), in this order: Z_32 and Z_68 (the
+// folds of a 136-B window's four chains), then Z_{136 * 2^k}, k = 0..3 (136 .. 1,088 B): a lane's
+// distance to the record end (k = 0..2), the Horner step over 8 windows (Z_1088), and the head's
+// shift past m - 1 windows by the bits of m - 1 (bits above 3 as repeated Z_1088).
+constexpr uint32_t kRingZN = 6;
 inline void build_ring_ztab(uint32_t *out) {
-    crc32c_shift_table(68, out);
-    for (uint32_t k = 0; k < kRingZN - 1; k++) crc32c_shift_table(136ull << k, out + 1024 * (k + 1));
+    crc32c_shift_table(32, out);
+    crc32c_shift_table(68, out + 1024);
+    for (uint32_t k = 0; k < 4; k++) crc32c_shift_table(136ull << k, out + 1024 * (k + 2));
 }
 
 }  // namespace bhg

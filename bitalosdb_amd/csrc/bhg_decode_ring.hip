@@ -24,16 +24,16 @@
 //     Consumers add to the slot's FREE word when done; the loader waits for it before reuse.
 //     Loads are non-temporal (the stream is read once).
 //   Consumer, per tile: lane (r, j) = record r of the tile, 8 lanes per record: the record's
-//     full 136-B windows counted from its end, window d on lane d % 8 (two 68-B chains folded
-//     with Z_68; Horner over a lane's windows with Z_1088; lane j shifted by Z_{136 j}; xor over
-//     the 8 lanes) -> crc_0 of the record minus its head (hl = L - 136 (m-1) bytes, 1..136).
+//     full 136-B windows counted from its end, window d on lane d % 8 (four chains of 36 + 32 +
+//     36 + 32 B folded with Z_32 and Z_68; Horner over a lane's windows with Z_1088; lane j
+//     shifted by Z_{136 j}; xor over the 8 lanes) -> crc_0 of the record minus its head (hl = L - 136 (m-1) bytes, 1..136).
 //     The head's 35 words are copied from LDS into the registers of the record's batch lane.
 //   Consumer, per batch (lane = record): head CRC from crc.New's ~0, shifted past the m-1 full
 //     windows (Z_{136 (m-1)} by the bits of m-1) and xored with the windows' part;
 //     readRecordHeader / readRecord / readKV / FNV-1 / trailer from the head words; expected
 //     CRC check; descriptor.  CRC linearity over GF(2): crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B).
-// CRC tables: CrcR8 (slice-by-4, 8 replicas, 32 KiB, conflict free) + 8 shift tables (32 KiB);
-// the ring (10 x 9 KiB) beside them: 155 KiB of LDS, one workgroup per CU.
+// CRC tables: CrcR8 (slice-by-4, 8 replicas, 32 KiB, conflict free) + 6 shift tables (24 KiB);
+// the ring (11 x 9 KiB) beside them: 156 KiB of LDS, one workgroup per CU.
 #include "bhg_crc_tables.h"
 #include "bhg_device.h"
 #include "bhg_internal.h"
@@ -43,9 +43,9 @@ namespace ring {
 
 constexpr uint32_t kNI = 9;                 // DMA wave instructions (1 KiB each) per tile
 constexpr uint32_t kSB = kNI * 1024;        // slot bytes
-constexpr uint32_t kNS = 10;                // ring slots
-constexpr uint32_t kD = 5;                  // tiles in flight behind the loader
-constexpr uint32_t kNC = 6;                 // consumer waves
+constexpr uint32_t kNS = 11;                // ring slots
+constexpr uint32_t kD = 4;                  // tiles in flight behind the loader
+constexpr uint32_t kNC = 7;                 // consumer waves
 constexpr uint32_t kMaxR = 8;               // records per tile
 constexpr uint32_t kW = 136;                // CRC window bytes
 constexpr uint32_t kQR = 8;                 // request ring entries per consumer
@@ -116,30 +116,34 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-// crc_0 of a 136-B window at LDS byte address a (4-aligned), as two 68-B chains folded with Z_68
-__device__ __forceinline__ uint32_t win_crc(const CrcR8 &crc, uint32_t z68, uint32_t a) {
-    uint32_t cA = 0, cB = 0;
+// crc_0 of a 136-B window at LDS byte address a (4-aligned) as four chains: words 0-8, 9-16, 17-25,
+// 26-33 (36 + 32 + 36 + 32 B), folded as Z_68(Z_32(cA) ^ cB) ^ (Z_32(cC) ^ cD): 9 dependent steps
+__device__ __forceinline__ uint32_t win_crc(const CrcR8 &crc, uint32_t z32, uint32_t z68, uint32_t a) {
+    uint32_t cA = 0, cB = 0, cC = 0, cD = 0;
 #pragma unroll
-    for (uint32_t t = 0; t < 17; t++) {
+    for (uint32_t t = 0; t < 9; t++) {
         cA = crc.word(cA, lds_ld32(a + 4 * t));
-        cB = crc.word(cB, lds_ld32(a + 68 + 4 * t));
+        if (t < 8) cB = crc.word(cB, lds_ld32(a + 36 + 4 * t));
+        cC = crc.word(cC, lds_ld32(a + 68 + 4 * t));
+        if (t < 8) cD = crc.word(cD, lds_ld32(a + 104 + 4 * t));
     }
-    return zshift(z68, cA) ^ cB;
+    return zshift(z68, zshift(z32, cA) ^ cB) ^ (zshift(z32, cC) ^ cD);
 }
 // the same at a byte address with a != 0 mod 4 (s = a & 3), from aligned words
-__device__ __forceinline__ uint32_t win_crc_u(const CrcR8 &crc, uint32_t z68, uint32_t a) {
+__device__ __forceinline__ uint32_t win_crc_u(const CrcR8 &crc, uint32_t z32, uint32_t z68, uint32_t a) {
     const uint32_t aa = a & ~3u, s = a & 3u;
-    uint32_t cA = 0, cB = 0;
-    uint32_t prevA = lds_ld32(aa), prevB = lds_ld32(aa + 68);
+    uint32_t w[35];
 #pragma unroll
-    for (uint32_t t = 0; t < 17; t++) {
-        const uint32_t nA = lds_ld32(aa + 4 * t + 4), nB = lds_ld32(aa + 68 + 4 * t + 4);
-        cA = crc.word(cA, __builtin_amdgcn_alignbyte(nA, prevA, s));
-        cB = crc.word(cB, __builtin_amdgcn_alignbyte(nB, prevB, s));
-        prevA = nA;
-        prevB = nB;
+    for (uint32_t t = 0; t < 35; t++) w[t] = lds_ld32(aa + 4 * t);
+    uint32_t cA = 0, cB = 0, cC = 0, cD = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 9; t++) {
+        cA = crc.word(cA, __builtin_amdgcn_alignbyte(w[t + 1], w[t], s));
+        if (t < 8) cB = crc.word(cB, __builtin_amdgcn_alignbyte(w[t + 10], w[t + 9], s));
+        cC = crc.word(cC, __builtin_amdgcn_alignbyte(w[t + 18], w[t + 17], s));
+        if (t < 8) cD = crc.word(cD, __builtin_amdgcn_alignbyte(w[t + 27], w[t + 26], s));
     }
-    return zshift(z68, cA) ^ cB;
+    return zshift(z68, zshift(z32, cA) ^ cB) ^ (zshift(z32, cC) ^ cD);
 }
 // crc_0 of a 136-B window at an absolute global address (big records), any alignment
 __device__ __forceinline__ uint32_t win_crc_g(const CrcR8 &crc, uint32_t z68, uint64_t a, uint64_t end) {
@@ -152,17 +156,30 @@ __device__ __forceinline__ uint32_t win_crc_g(const CrcR8 &crc, uint32_t z68, ui
     return zshift(z68, cA) ^ cB;
 }
 
-template <int DUMMY = 0>
+// KO: timing-only knock-outs for the lab (0 in the product): 1 window CRCs, 2 head copies,
+// 4 the batch parse, 8 all tile work
+template <int KO = 0>
 __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *__restrict__ src, uint64_t src_len,
                                                                 const bhg_handle *__restrict__ handles, uint32_t n,
                                                                 const uint32_t *__restrict__ expected_crc,
                                                                 bhg_desc *__restrict__ out,
                                                                 const uint32_t *__restrict__ rz,
-                                                                uint32_t *__restrict__ err) {
+                                                                uint32_t *__restrict__ err,
+                                                                unsigned long long *__restrict__ prof = nullptr) {
+    // KO & 16 (lab): per-phase shader-clock totals, prof[0..3] loader, prof[4..7] consumers
+    unsigned long long pt[4] = {0, 0, 0, 0};
+    auto clk = [&]() -> unsigned long long { return (KO & 16) ? (unsigned long long)__builtin_amdgcn_s_memtime() : 0ull; };
+    const unsigned long long t_start = clk();
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     const uint32_t lb = lds_addr(lds);
     const uint32_t zb = lb + kOffZ;
-    const uint32_t Z68 = zb, Z136 = zb + 4096, Z1088 = zb + 4 * 4096;
+    const uint32_t Z32 = zb, Z68 = zb + 4096, Z136 = zb + 2 * 4096, Z1088 = zb + 5 * 4096;
+    // Z_{136 * 2^bt}: a table for bt <= 3, repeated Z_1088 above
+    auto zwin = [&](uint32_t bt, uint32_t c) {
+        if (bt <= 3) return zshift(Z136 + bt * 4096, c);
+        for (uint32_t q = 0; q < (1u << (bt - 3)); q++) c = zshift(Z1088, c);
+        return c;
+    };
     const uint32_t ring = lb + kOffRing, reqb = lb + kOffReq, mailb = lb + kOffMail, freeb = lb + kOffFree;
     const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
     const uint64_t base = (uint64_t)src, end = base + src_len;
@@ -198,15 +215,17 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
             const uint32_t c = e & 7, s = (e >> 3) & 15, sq = e >> 8;
             put32(mailb + 4 * (c * kQM + ((sq - 1) & (kQM - 1))), (sq << 8) | s);
         };
+        static_assert(kNC * kQR <= 64, "one request word per loader lane");
         while (live != 0 || nout != 0) {
             bool prog = false;
+            // every request word at once: lane c * kQR + q holds consumer c's entry q
+            uint64_t ev;
+            const uint32_t ra = reqb + 8 * (lane < kNC * kQR ? lane : 0u);
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(ev) : "v"(ra) : "memory");
 #pragma unroll
             for (uint32_t c = 0; c < kNC; c++) {
                 if (!((live >> c) & 1)) continue;
-                uint64_t e;
-                const uint32_t a = reqb + 8 * (c * kQR + (kreq[c] & (kQR - 1)));
-                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(a) : "memory");
-                e = readfirstlane_u64(e);
+                const uint64_t e = readlane_u64(ev, (int)(c * kQR + (kreq[c] & (kQR - 1))));
                 const uint32_t sq = (uint32_t)(e >> 56);
                 if (sq != ((kreq[c] + 1) & 0xff)) continue;
                 kreq[c]++;
@@ -218,6 +237,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                 const uint32_t s = T % kNS;
                 if (T >= kNS) {
                     uint32_t sp = 0;
+                    const unsigned long long t0 = clk();
                     while (poll32(freeb + 4 * s) < T / kNS) {
                         if (poll32(lb + kOffErr) != 0) break;
                         __builtin_amdgcn_s_sleep(1);
@@ -226,6 +246,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                             break;
                         }
                     }
+                    pt[0] += clk() - t0;
                 }
                 const uint64_t B = (e & ((1ull << 44) - 1)) << 4;
                 const uint32_t np = (uint32_t)((e >> 44) & 1023) << 0;  // pieces (bytes >> 4)
@@ -247,7 +268,9 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                 // kD tiles in flight: the oldest has landed once all but the newest kNI * (kD - 1)
                 // loads are done; at most kD - 1 = 4 entries live in the 64-bit FIFO
                 if (nout == kD - 1) {
+                    const unsigned long long t0 = clk();
                     wait_vm<kNI * (kD - 1)>();
+                    pt[1] += clk() - t0;
                     publish((uint32_t)(fifo >> (16 * (kD - 2))) & 0xffffu);
                     nout--;
                 }
@@ -259,10 +282,13 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
             if (prog) {
                 idle = 0;
             } else if (nout != 0) {  // no request waiting: land and mail everything in flight
+                const unsigned long long t0 = clk();
                 wait_vm<0>();
+                pt[2] += clk() - t0;
                 for (uint32_t q = nout; q > 0; q--) publish((uint32_t)(fifo >> (16 * (q - 1))) & 0xffffu);
                 nout = 0;
             } else {
+                pt[3] += 1;
                 __builtin_amdgcn_s_sleep(2);
                 if (++idle >= kSpin || poll32(lb + kOffErr) != 0) {
                     put32(lb + kOffErr, 2u);
@@ -394,6 +420,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                 // the tile's slot
                 const uint32_t want = (kproc + 1) & 0xff;
                 uint32_t m = 0, sp = 0;
+                const unsigned long long tm0 = clk();
                 while (((m = poll32(mymail + 4 * (kproc & (kQM - 1)))) >> 8) != want) {
                     if (poll32(lb + kOffErr) != 0) break;
                     __builtin_amdgcn_s_sleep(1);
@@ -402,13 +429,16 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                         break;
                     }
                 }
+                const unsigned long long tm1 = clk();
+                pt[0] += tm1 - tm0;
                 const uint32_t s = m & 15;
                 const uint32_t sl = ring + s * kSB;
                 const uint64_t B = readlane_u64(cur.p, (int)ts) & ~15ull;
                 const uint32_t Lts = (uint32_t)__builtin_amdgcn_readlane((int)cur.L, (int)ts);
                 const uint64_t e16ts = readlane_u64((cur.p + cur.L + 15) & ~15ull, (int)ts);
                 const bool big = Lts != 0 && e16ts - B > kSB;
-                if (!big) {
+                if (KO & 8) {
+                } else if (!big) {
                     // ---- window CRCs, lane (rr, j) on record ts + rr
                     const uint32_t ri = ts + rr;
                     const bool act = ri < te;
@@ -423,10 +453,11 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                     const bool wal = __ballot(d >= 0 && (E & 3) != 0) == 0;
                     uint32_t acc = 0;
                     bool first = true;
+                    if (KO & 1) d = -1;
                     while (__ballot(d >= 0)) {
                         if (d >= 0) {
                             const uint32_t a = E - kW * (uint32_t)(d + 1);
-                            const uint32_t V = wal ? win_crc(crc, Z68, a) : win_crc_u(crc, Z68, a);
+                            const uint32_t V = wal ? win_crc(crc, Z32, Z68, a) : win_crc_u(crc, Z32, Z68, a);
                             acc = first ? V : (zshift(Z1088, acc) ^ V);
                             first = false;
                             d -= 8;
@@ -443,7 +474,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                     const uint32_t got = __shfl(acc, srcl & 63, 64);
                     if (lane >= ts && lane < te) {
                         wpart = got;
-                        if (cur.L != 0) {
+                        if (cur.L != 0 && !(KO & 2)) {
                             const uint32_t ha = (sl + (uint32_t)(cur.p - B)) & ~3u;
 #pragma unroll
                             for (uint32_t u = 0; u < 35; u++) hw[u] = lds_ld32(ha + 4 * u);
@@ -468,14 +499,15 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                             } else {
                                 V = win_crc_g(crc, Z68, eb - kW * (uint64_t)(d + 1), end);
                             }
-                            acc = first ? V : (zshift(zb + 7 * 4096, acc) ^ V);
+                            if (!first) acc = zwin(6, acc);  // Z_8704: 64 windows
+                            acc = first ? V : (acc ^ V);
                             first = false;
                             d -= 64;
                         }
                     }
 #pragma unroll
                     for (uint32_t bt = 0; bt < 6; bt++)
-                        if ((lane >> bt) & 1) acc = zshift(Z136 + bt * 4096, acc);
+                        if ((lane >> bt) & 1) acc = zwin(bt, acc);
 #pragma unroll
                     for (uint32_t o = 1; o < 64; o <<= 1) acc ^= __shfl_xor(acc, o, 64);
                     if (lane == ts) {
@@ -487,9 +519,11 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                     }
                 }
                 release(freeb + 4 * s);
+                pt[1] += clk() - tm1;
                 kproc++;
             }
             // ---- batch end: lane = record b0 + lane
+            const unsigned long long tp0 = clk();
             {
                 const bool valid = lane < cnt;
                 const uint32_t L = cur.L, st = cur.st;
@@ -499,7 +533,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
 #pragma unroll
                 for (int u = 0; u < 34; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
                 uint32_t fullc = 0;
-                if (inb) {
+                if (inb && !(KO & 4)) {
                     if (bigdone) {
                         fullc = wpart;
                     } else {
@@ -518,7 +552,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                         const uint32_t sft = mw - 1;  // <= 67 for records that fit a slot
 #pragma unroll
                         for (uint32_t bt = 0; bt < 7; bt++)
-                            if ((sft >> bt) & 1) hc = zshift(Z136 + bt * 4096, hc);
+                            if ((sft >> bt) & 1) hc = zwin(bt, hc);
                         fullc = hc ^ wpart;
                     }
                 }
@@ -526,7 +560,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                 uint32_t k = 0, v = 0, fn = 0, key_len = 0, fnv = BHG_FNV_OFFSET;
                 uint64_t trailer = 255;  // InternalKeyKindInvalid when ikeySize < 8
                 bool rvalid = false;
-                if (inb) {
+                if (inb && !(KO & 4)) {
                     k = L >= 12 ? rw[0] : 0u;
                     v = L >= 12 ? rw[1] : 0u;
                     fn = L >= 12 ? rw[2] : 0u;
@@ -580,6 +614,7 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
                     __builtin_nontemporal_store((uint64_t)dcrc | ((uint64_t)dst << 32), o + 4);
                 }
             }
+            pt[2] += clk() - tp0;
             // advance: the next batch becomes current (its unposted tiles stay unposted)
             cur = nxt;
             nxt = nn;
@@ -591,6 +626,11 @@ __global__ __launch_bounds__(64 * (kNC + 1)) void k_decode_ring(const uint8_t *_
             nxt_rem_post = pmn;
         }
         if (!term) put64(myreq + 8 * (kpost & (kQR - 1)), kReqTerm | ((uint64_t)((kpost + 1) & 0xff) << 56));
+    }
+    if ((KO & 16) && prof != nullptr && lane == 0) {
+        const uint32_t o = wv == 0 ? 0u : 4u;
+        for (int q = 0; q < 4; q++) atomicAdd(prof + o + q, pt[q]);
+        atomicAdd(prof + 8 + (wv == 0 ? 0 : 1), clk() - t_start);
     }
     __syncthreads();
     if (threadIdx.x == 0) {

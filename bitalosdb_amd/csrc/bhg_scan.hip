@@ -117,7 +117,6 @@ size_t scan_scratch_bytes(uint64_t n) {
     return bytes + 64;
 }
 
-// exclusive scan of in[0..n) into out[0..n], out[n] = total.  in may equal out.
 // p[i * stride] += add (mod 2^64) over n entries: the pipelined snappy host path rebases a chunk's
 // scanned value offsets onto the batch (stride 1) and its handles onto the chunk's staged bytes
 // (stride 2: bhg_handle.offset, add = -lo)
@@ -165,6 +164,7 @@ hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, ui
     return hipGetLastError();
 }
 
+// exclusive scan of in[0..n) into out[0..n], out[n] = total.  in may equal out.
 hipError_t launch_exclusive_scan_u64(const Launch &L, const uint64_t *in, uint64_t *out, uint64_t n, void *scratch) {
     if (n == 0) {
         return hipMemsetAsync(out, 0, sizeof(uint64_t), L.stream);

@@ -378,6 +378,10 @@ int bhg_get_batch(bhg_ctx *ctx, const uint8_t *src, uint64_t src_len, const bhg_
  * the AddIkey khash).  Writer.Get (writer.go:171-228) on it: a khash whose adds all carried one
  * UserKey answers the last add (ih.bh, whatever key is queried, as Go does); two or more
  * distinct keys (conflict) answer the last add of the queried key (conflictKeys) or nothing.
+ * Assumption: one khash per UserKey (Writer.Add's hash.Fnv32, and every AddIkey caller in the
+ * reference).  Go's conflictKeys is one map per writer, so a key added under two khash values
+ * whose runs both conflict answers its last add in either run; here it answers its last add in
+ * the queried run.
  *   rec       : device bhg_handle[n], the records in add order (offsets into src)
  *   sorted    : device uint32_t[n] record indices sorted by khash
  *   sorted_kh : device uint32_t[n] khash of sorted[j]

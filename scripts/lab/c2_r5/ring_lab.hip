@@ -101,12 +101,13 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&rz, z.size() * 4));
     CK(hipMemcpy(rz, z.data(), z.size() * 4, hipMemcpyHostToDevice));
     CK(hipMalloc(&err, 4));
-    CK(hipMemset(err, 0, 4));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     int fails = 0;
-    for (int which = 0; which < 3; which++) {
+    const int nsets = argc > 3 ? atoi(argv[3]) : 3;  // 1: the C2 set only (profiling runs)
+    const bool quick = argc > 4;                     // no knock-out / clock-profile variants
+    for (int which = 0; which < nsets; which++) {
         Set st = which == 2 ? make_mixed(n / 4) : make_c2(n);
         const char *name = which == 0 ? "c2" : which == 1 ? "shuf" : "mixed";
         if (which == 1) std::shuffle(st.h.begin(), st.h.end(), rng);
@@ -124,7 +125,7 @@ int main(int argc, char **argv) {
         }
         auto prod = [&]() { if (bhg_decode_batch(ctx, src, len, dh, nn, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
         auto ringk = [&]() {
-            hipLaunchKernelGGL((ring::k_decode_ring<0>), dim3(cus), dim3(64 * (ring::kNC + 1)), 0, s, src, len, dh, nn, ec, o2, rz, err);
+            hipLaunchKernelGGL((ring::k_decode_ring<0>), dim3(cus), dim3(64 * (ring::kNC + 1)), 0, s, src, len, dh, nn, ec, o2, rz, err, (unsigned long long *)nullptr);
         };
         for (int it = 0; it < 50; it++) prod();  // clocks
         CK(hipStreamSynchronize(s));
@@ -156,6 +157,36 @@ int main(int argc, char **argv) {
         const double alg = (double)tot + 60.0 * nn;  // record bytes + handle + expected CRC + descriptor
         auto tp = timeit(prod);
         auto tr = timeit(ringk);
+        if (which == 0 && !quick) {
+            auto ko = [&](auto kern, const char *nm) {
+                auto t = timeit([&]() { hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * (ring::kNC + 1)), 0, s, src, len, dh, nn, ec, o2, rz, err, (unsigned long long *)nullptr); });
+                printf("   ko %-22s %.4f ms (frac-equiv %.4f)\n", nm, t.first, alg / (t.first * 1e-3) / 8e12);
+            };
+            ko(ring::k_decode_ring<1>, "no window CRC");
+            ko(ring::k_decode_ring<2>, "no head copy");
+            ko(ring::k_decode_ring<4>, "no parse");
+            ko(ring::k_decode_ring<7>, "none of the three");
+            ko(ring::k_decode_ring<8 | 4>, "protocol only");
+            unsigned long long *prof;
+            CK(hipMalloc(&prof, 16 * 8));
+            auto prun = [&](auto kern, const char *nm) {
+                CK(hipMemset(prof, 0, 16 * 8));
+                hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * (ring::kNC + 1)), 0, s, src, len, dh, nn, ec, o2, rz, err, prof);
+                CK(hipStreamSynchronize(s));
+                unsigned long long h[16];
+                CK(hipMemcpy(h, prof, 16 * 8, hipMemcpyDeviceToHost));
+                const double Lw = (double)h[8] / cus, Cw = (double)h[9] / (cus * ring::kNC);
+                printf("   prof %-12s loader total %.0f clk: FREE-wait %.1f%% vm-wait %.1f%% drain %.1f%% idle-iters %.0f | "
+                       "consumer total %.0f: mail-wait %.1f%% tile %.1f%% parse %.1f%%\n", nm, Lw, 100.0 * h[0] / cus / Lw,
+                       100.0 * h[1] / cus / Lw, 100.0 * h[2] / cus / Lw, (double)h[3] / cus, Cw,
+                       100.0 * h[4] / (cus * ring::kNC) / Cw, 100.0 * h[5] / (cus * ring::kNC) / Cw,
+                       100.0 * h[6] / (cus * ring::kNC) / Cw);
+            };
+            prun(ring::k_decode_ring<16>, "full");
+            prun(ring::k_decode_ring<16 | 1>, "no-winCRC");
+            prun(ring::k_decode_ring<16 | 8 | 4>, "protocol");
+            CK(hipFree(prof));
+        }
         CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
         printf("%-6s n=%u ok=%u  product %.4f ms (frac %.4f)  ring %.4f ms best %.4f (frac %.4f)  mismatches %u (first %u) err %u\n",
                name, nn, nok, tp.first, alg / (tp.first * 1e-3) / 8e12, tr.first, tr.second, alg / (tr.first * 1e-3) / 8e12,
