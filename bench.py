@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes that measure roofline.traffic (N=1, rank 0)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "scan", "scanmix", "get",
-                                                       "indexcrc", "tail", "spawncheck"],
+                                                       "indexcrc", "tail", "mixdec", "spawncheck"],
                     help="c1: 100k blocks on the host CPU; c2: uncompressed decode (BASELINE metric; at N > 1 "
                          "the line is the C5 strong-scaling corpus); c3: snappy decode; c4: encode; "
                          "c5: 25 GB corpus sharded round-robin by table over the GPUs (strong scaling); "
@@ -76,6 +76,8 @@ def parse():
                          "indexcrc: per-table indexhash_checksum verify (masked CRC-32C of 1.51 MB per table); "
                          "tail: Writer.writeTable's tail (bhg_table_tail) for 1M records as 8 tables of 128 MiB "
                          "and as ONE table of 1M records (natural FNV-1 collisions -> a conflict block); "
+                         "mixdec: decode of C4-shaped tables (1M pairs, values U[64, 4096] B), snappy line with "
+                         "the NoCompressor line nested; "
                          "spawncheck: no GPU -- the --gpus N launch path alone (rank env, gloo rendezvous, "
                          "the all-reduce that reports ranks_seen, rank 0's JSON line), for CPU tests")
     return ap.parse_args()
@@ -354,6 +356,8 @@ def run(a, world, rank, local, dev, codec):
         return run_indexcrc(a, world, rank, local, dev, codec)
     if a.config == "tail":
         return run_tail(a, world, rank, local, dev, codec)
+    if a.config == "mixdec":
+        return run_mixdec(a, world, rank, local, dev, codec)
     if a.config == "c5":
         return run_c5(a, world, rank, local, dev, codec)
     if a.config == "c1":
@@ -909,6 +913,83 @@ def c4_measure(a, world, rank, local, dev, codec, gen, extras):
                                          "pairs on 1 thread (%s)" % (n, reps, cs, thr, m1, cpu_info())}
         res["parity_first_%d" % m] = "bit-exact" if par else "MISMATCH"
     return res
+
+
+def run_mixdec(a, world, rank, local, dev, codec):
+    """Decode of the C4-shaped tables (SURVEY 8(d) C4 value mix: 1M pairs, values U[64, 4096] B of
+    the --values generator, as BithashWriter.Add writes them): the snappy line, with the
+    NoCompressor decode of the same pairs nested.  Reader.readData decodes any value length
+    (reader.go:233-272); this is the shape outside the 1 KiB benchmark values."""
+    out = mixdec_measure(a, world, rank, local, dev, codec, 1, extras=True)
+    torch.cuda.empty_cache()
+    nc = mixdec_measure(a, world, rank, local, dev, codec, 0, extras=True)
+    out["nocompressor"] = {k: nc[k] for k in ("value", "unit", "ms_per_step", "roofline", "status_ok_blocks",
+                                               "parity_first_blocks", "valid")}
+    out["nocompressor"].update(nc["config"])
+    out["valid"] = bool(out["valid"] and nc["valid"])
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def mixdec_measure(a, world, rank, local, dev, codec, compressor, extras):
+    from bitalosdb_amd.codec import handles_tensor
+    n = a.blocks
+    g = torch.Generator(device=dev)
+    g.manual_seed(synth_seed(rank) + 7)
+    val_lens = torch.randint(64, 4097, (n,), generator=g, device=dev, dtype=torch.int64)
+    src, h, meta, enc = _encode_tables(codec, n, val_lens, dev, synth_seed(rank), compressor, a.values)
+    exp_crc = enc[-1].crc
+    h_t = handles_tensor(h, dev)
+    desc = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    dec_total = int(val_lens.sum().item())
+    if compressor:
+        voff = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev)
+        vals = torch.empty(dec_total + 64, dtype=torch.uint8, device=dev)
+        step = lambda: codec.decode_batch(src, src.numel(), h_t, n, 1, expected_crc=exp_crc, out_desc=desc,
+                                          out_vals=vals, out_val_off=voff)
+    else:
+        step = lambda: codec.decode_batch(src, src.numel(), h_t, n, 0, expected_crc=exp_crc, out_desc=desc)
+    el, kms = _timed(a, dev, step)
+    d = desc.cpu().numpy().view(DESC_DT)
+    disk = float(h["length"].astype(np.float64).sum())
+    lens = val_lens.cpu().numpy()
+    name = "snappy" if compressor else "NoCompressor"
+    out = {"metric": "GiB/s bithash blocks decoded (device-resident), %s, C4 value mix 64B-4KB, 1 GPU" % name,
+           "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (GPU-encoded %s tables, values: %s)" % (name, a.values),
+           "config": {"workload": "decode of the C4-shaped tables: 1M pairs, 32 B keys, values U[64, 4096] B, "
+                                  "CRC-verify (the writer's CRCs) + %sdecode" % ("decompress + " if compressor else ""),
+                      "codec": name, "values": a.values, "blocks_per_gpu": n, "mean_record_bytes": round(disk / n, 1),
+                      "decoded_value_bytes": dec_total,
+                      "decoded_GiBps": round(dec_total * a.steps / el / 2 ** 30, 3)},
+           "status_ok_blocks": int((d["status"] == 0).sum())}
+    if compressor:
+        # k_snappy_lds takes blocks that decode to <= 1 KiB (bhg_snappy_dec.hip); the rest go to k_snappy_rt
+        out["config"]["blocks_decoding_over_1KiB"] = int((lens > 1024).sum())
+        out["config"]["share_over_1KiB"] = round(float((lens > 1024).mean()), 4)
+    out["valid"] = out["status_ok_blocks"] == n
+    alg = n * (16 + 4 + 40) + disk + (dec_total if compressor else 0)
+    out["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "traffic": None, "scope": "whole step (event-timed)", "step_event_ms": round(kms, 4),
+                       "algorithmic": "handle 16 + record + expected CRC 4 + descriptor 40%s per block" %
+                                      (" + decoded value" if compressor else "")}
+    if extras and rank == 0 and world == 1:
+        # parity: the first 20k blocks against the restated decode (oracle/bithash_oracle.c)
+        from oracle import oracle as O
+        m = min(n, 20000)
+        host = src.cpu().numpy()
+        ecrc = exp_crc.cpu().numpy().view(np.uint32)
+        exp, ev, eo = O.decode_batch(host, h[:m], codec=compressor, expected_crc=ecrc[:m], nthreads=usable_cores())
+        par = all(np.array_equal(exp[f], d[:m][f]) for f in d.dtype.names)
+        if compressor:
+            got_v = vals.cpu().numpy()
+            par = par and got_v[:int(eo[-1])].tobytes() == ev[:int(eo[-1])].tobytes()
+        out["parity_first_blocks"] = "%s (%d blocks)" % ("bit-exact" if par else "MISMATCH", m)
+        out["valid"] = bool(out["valid"] and par)
+    return out
 
 
 C5_RECORDS_PER_TABLE = 124_738      # 128 MiB / 1076 B, the add that crosses the limit included
