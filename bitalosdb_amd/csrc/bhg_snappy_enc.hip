@@ -20,7 +20,7 @@ namespace bhg {
 
 typedef u32x4 u32x4u __attribute__((aligned(1)));
 // Tuning constants, each measured (lab records under profiles/r2*, r3/enc*):
-constexpr uint32_t kSeDcnt = 256;  // dwords of byte counters for the in-batch duplicate check (4 buckets each)
+constexpr uint32_t kSeDcnt = 272;  // dwords of the in-batch duplicate check: 1,024 bucket bytes + 64 lane bytes
 constexpr uint32_t kSeHeads = 8;   // queue heads per class list
 constexpr uint32_t kSeStatic = 75; // % of a class list handed out round-robin before the work queue takes over
 constexpr int kSeWpg = 3;          // waves per workgroup of the large-value launch
@@ -247,19 +247,23 @@ template <uint32_t DUMMY>
 __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                                              uint32_t nl, bool valid, uint64_t vmask, uint32_t pos, uint32_t u, uint32_t h,
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
-    // lanes that may share a bucket: per-bucket counts of h mod 1024, one byte per bucket
-    // (<= 64 adds per byte); only those lanes are walked
-    const uint32_t slot = (h >> 2) & (kSeDcnt - 1u), sh8 = 8 * (h & 3);
-    const uint32_t one = valid ? 1u << sh8 : 0u;
-    atomicAdd(&dcnt[slot], one);  // unconditional: no exec-mask branch
+    // lanes whose bucket (h mod 1024) a HIGHER lane of the batch shares: every lane writes its
+    // lane number + 1 into the bucket's byte and reads it back -- in one LDS store instruction the
+    // highest lane's byte is the one that stays, so exactly the lanes below another lane of their
+    // bucket read a foreign byte (the highest lane of a bucket has no lane above it to hand its
+    // position to, and nothing to learn from the walk: its nxt stays 64).  Invalid lanes write
+    // into their own scratch bytes.  Two LDS operations, no atomics (the per-bucket counters
+    // before: add, read, subtract).
+    uint8_t *const db = reinterpret_cast<uint8_t *>(dcnt);
+    const uint32_t bidx = valid ? (h & 1023u) : 1024u + lane;
+    db[bidx] = (uint8_t)(lane + 1);
     wsync();
-    const uint32_t cnt = dcnt[slot];
+    const uint32_t got = db[bidx];
     wsync();
-    atomicSub(&dcnt[slot], one);
     // (lane predicates combined as 64-bit masks: a ballot of a combined bool re-materialises it
     // in a VGPR, two VALU each)
     const uint64_t vm = vmask;
-    const uint64_t dm0 = vm & bal(((cnt >> sh8) & 0xffu) > 1);
+    const uint64_t dm0 = vm & bal(got != lane + 1);
 #ifdef BHG_SE_PROF
     acc[6] += 1;
     acc[7] += __builtin_popcountll(dm0);
