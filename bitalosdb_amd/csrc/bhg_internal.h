@@ -59,12 +59,13 @@ void build_stream_tab_default(uint32_t *out);
 hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                                 int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
 // bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
-// list: device scratch of snappy_list_bytes(n) (the blocks the LDS decoder hands to the
-// global-memory pass); null -> every block through the global-memory kernel
+// list: device scratch of snappy_list_bytes(n) (the blocks each LDS tier hands to the
+// next: 1-KiB slots -> 4-KiB slots -> global memory); null -> every block through the
+// global-memory kernel
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list);
-inline size_t snappy_list_bytes(uint32_t n) { return 4 + 4 * (size_t)n; }
+inline size_t snappy_list_bytes(uint32_t n) { return 8 + 8 * (size_t)n; }
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)

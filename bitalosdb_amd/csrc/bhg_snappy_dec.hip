@@ -161,17 +161,18 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
 
 }  // namespace
 
-// list: null (every block) or {count, block indices...} (the blocks k_snappy_lds left)
+// list_cnt/list_ent: null (every block) or the count and block indices k_snappy_lds left
 __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off,
-                                                   const uint32_t *__restrict__ list) {
+                                                   const uint32_t *__restrict__ list_cnt,
+                                                   const uint32_t *__restrict__ list_ent) {
     const uint64_t base = (uint64_t)src, end = base + src_len;
     const uint64_t oend = (uint64_t)out_vals + out_cap;
-    const uint32_t cnt = list ? list[0] : n;
+    const uint32_t cnt = list_cnt ? *list_cnt : n;
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
-        const uint32_t i = list ? list[1 + j] : j;
+        const uint32_t i = list_ent ? list_ent[j] : j;
         uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
         const uint32_t status = dw[9];
         if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
@@ -240,6 +241,9 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSlBpw = 18;     // blocks (lanes) per wave
 constexpr uint32_t kSlSlot = 1088;  // in-place slot bytes per block
+constexpr uint32_t kSlBpw2 = 6;      // tier 2 (values up to 4 KiB)
+constexpr uint32_t kSlSlot2 = 4160;
+constexpr uint32_t kSlCh2 = 2;
 
 // Every LDS access of k_snappy_lds goes through these may_alias types: the slot
 // is written as 16-B chunks and read as bytes, 8-B tags and 16-B chunks, and
@@ -264,7 +268,7 @@ enum : uint32_t { SL_SKIP = 0, SL_LDS = 1, SL_GLOBAL = 2, SL_TOOLARGE = 3 };
 
 struct SlInfo {
     uint64_t cp, o0;  // stream (absolute, varint header included), output offset in out_vals
-    uint32_t clen, dlen, status, mode;
+    uint32_t clen, dlen, status, mode, i;
 };
 
 // in-place slot: where a stream of clen bytes is staged (16-B aligned, 8 B of
@@ -306,12 +310,13 @@ __device__ __forceinline__ SlInfo sl_finish(const SlRaw &w, uint32_t n, uint64_t
     r.clen = w.hlen - w.cpos;
     r.dlen = w.dlen;
     r.status = w.st;
+    r.i = w.i;
     if (w.i >= n || (w.st != BHG_ST_OK && w.st != BHG_ST_CRC_MISMATCH))
         r.mode = SL_SKIP;
     else if (w.o1 > out_cap || w.o1 - w.o0 < w.dlen)
         r.mode = SL_TOOLARGE;
     else
-        r.mode = (w.dlen <= 1024u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
+        r.mode = (w.dlen <= (uint32_t)SLOT - 64u && r.clen + 24u <= (uint32_t)SLOT) ? SL_LDS : SL_GLOBAL;
     return r;
 }
 
@@ -386,77 +391,112 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 
 }  // namespace
 
-template <int BPW, int SLOT>
+// Two tiers of the same kernel: <18, 1,088, 1> takes every block (values that
+// decode to <= 1 KiB), <6, 4,160, 2> the blocks tier 1 listed (values up to
+// 4 KiB, and tier-1 spills), and k_snappy_rt the rest.  in_cnt/in_ent
+// (LISTED false: every block) or the list to take; out_cnt/out_ent: where
+// blocks that do not fit are listed.  CH: 16-B stream chunks per lane per
+// block prefetched into VGPRs (the rest of a longer stream is loaded at the
+// dump).
+// Measured on the C4-shaped decode (bench.py --config mixdec: 1M values
+// U[64, 4096], 76 % of them > 1 KiB): the > 1 KiB blocks took 5.83 ms per
+// step in k_snappy_rt; tier 2 takes 4.2 ms (step 6.90 -> 5.27 ms, 137 -> 180
+// GiB/s).  Tier-2 shapes A/B'd (2 runs each, one box; profiles/r5/snappy_t2):
+// 6 blocks x 2 chunks 5.27 ms, 4 x 4 5.44, 3 x 4 5.52, 2 x 4 5.77; 64-B ops
+// (4 reads in flight per element) 6.3 ms and C3 +12 %; a 2-KiB class of 12
+// (or 9, 16) blocks per wave for values <= 2 KiB 5.30-5.47 ms; one WAVE per
+// block (wave-uniform SALU decode, byte-per-lane copies) 7.3 ms for tier 2
+// alone -- 73 SALU instructions per element for one block, where a lane walk
+// spends ~80 VALU per element step for 6.
+template <int BPW, int SLOT, int CH, bool LISTED>
 __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off,
-                                                   uint32_t *__restrict__ list) {
+                                                   const uint32_t *__restrict__ in_cnt,
+                                                   const uint32_t *__restrict__ in_ent, uint32_t *__restrict__ out_cnt,
+                                                   uint32_t *__restrict__ out_ent) {
     static_assert(SLOT % 16 == 0, "16-B aligned slots");
+    constexpr uint32_t DMAX = SLOT - 64;            // longest decoded block a slot takes
+    constexpr uint32_t DCH = (DMAX + 1023) / 1024;  // 1-KiB rows of the store-out
     __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint32_t ngroups = (n + BPW - 1) / BPW;
+    const uint32_t cnt = LISTED ? *in_cnt : n;
+    const uint32_t ngroups = (cnt + BPW - 1) / BPW;
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
-    auto load = [&](uint32_t grp) -> SlRaw {
-        const uint32_t i = grp * BPW + lane;
-        return sl_load(lane < BPW && grp < ngroups ? i : n, n, out, handles, val_off);
+    // block index of this lane in group grp (n: none); listed: one load, issued a group before
+    // the descriptor loads that need it
+    auto index = [&](uint32_t grp) -> uint32_t {
+        const uint32_t j = grp * BPW + lane;
+        const bool ok = lane < BPW && grp < ngroups && j < cnt;
+        if (!LISTED) return ok ? j : n;
+        const uint32_t x = in_ent[ok ? j : 0u];  // cnt >= 1 here
+        return ok ? x : n;
     };
-    auto info = [&](uint32_t grp) -> SlInfo { return sl_finish<SLOT>(load(grp), n, base, out_cap); };
-    u32x4 v[BPW];
-    // One 16-B chunk per lane per staged block, loaded unconditionally (lanes
+    auto load = [&](uint32_t i) -> SlRaw { return sl_load(i < n ? i : n, n, out, handles, val_off); };
+    u32x4 v[BPW * CH];
+    // CH 16-B chunks per lane per staged block, loaded unconditionally (lanes
     // past the stream load src + 0; the dump drops them) and clamped to end
     // src (a chunk that would cross the end is loaded from end - 16 and
     // shifted into place at the dump), so no branch and no wait is tied to the
     // loads until the next dump.  (The launcher sends src_len < 64 elsewhere.)
-    auto chunk_addr = [&](const SlInfo &I, int b, uint32_t &clb) -> uint64_t {
-        clb = __builtin_amdgcn_readlane(I.mode == SL_LDS ? I.clen : 0u, b);
-        const uint64_t cpb = readlane_u64(I.cp, b);
-        return 16 * lane < clb ? cpb + 16 * lane : base;
-    };
     auto prefetch = [&](const SlInfo &I) {
 #pragma unroll
         for (int b = 0; b < BPW; b++) {
-            uint32_t clb;
-            const uint64_t a = chunk_addr(I, b, clb);
-            v[b] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
+            const uint32_t clb = __builtin_amdgcn_readlane(I.mode == SL_LDS ? I.clen : 0u, b);
+            const uint64_t cpb = readlane_u64(I.cp, b);
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const uint32_t off = 1024u * c + 16u * lane;
+                const uint64_t a = off < clb ? cpb + off : base;
+                v[b * CH + c] = gld<u32x4u>(a + 16 <= end ? a : end - 16);
+            }
         }
     };
-    SlInfo cur = info(g);
+    SlInfo cur = sl_finish<SLOT>(load(index(g)), n, base, out_cap);
     prefetch(cur);
-    SlInfo nxt = info(g + G);
+    SlInfo nxt = sl_finish<SLOT>(load(index(g + G)), n, base, out_cap);
+    uint32_t ix2 = index(g + 2 * G);
     for (; g < ngroups; g += G) {
         // 1. this group's streams -> slots
 #pragma unroll
         for (int b = 0; b < BPW; b++) {
-            uint32_t clb;
-            const uint64_t a = chunk_addr(cur, b, clb);
-            u32x4 c = v[b];
-            if (a + 16 > end) {  // the chunk was loaded from end - 16: its bytes start at a - (end - 16)
-                const uint32_t sh = (uint32_t)(a - (end - 16));
-                unsigned __int128 x = (unsigned __int128)c.x | ((unsigned __int128)c.y << 32) |
-                                      ((unsigned __int128)c.z << 64) | ((unsigned __int128)c.w << 96);
-                x >>= 8 * sh;
-                c = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+            const uint32_t clb = __builtin_amdgcn_readlane(cur.mode == SL_LDS ? cur.clen : 0u, b);
+            const uint64_t cpb = readlane_u64(cur.cp, b);
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const uint32_t off = 1024u * c + 16u * lane;
+                const uint64_t a = cpb + off;
+                u32x4 x4 = v[b * CH + c];
+                if (off < clb && a + 16 > end) {  // the chunk was loaded from end - 16: its bytes start at a - (end - 16)
+                    const uint32_t sh = (uint32_t)(a - (end - 16));
+                    unsigned __int128 x = (unsigned __int128)x4.x | ((unsigned __int128)x4.y << 32) |
+                                          ((unsigned __int128)x4.z << 64) | ((unsigned __int128)x4.w << 96);
+                    x >>= 8 * sh;
+                    x4 = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+                }
+                if (off < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + off) = x4;
             }
-            if (16 * lane < clb) *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 16 * lane) = c;
         }
-        // streams past 64 chunks (1,025 .. SLOT - 24 B: values snappy could not shrink, ~1 in
-        // 3,000 dict values): the rest loaded here, synchronously -- rare, and it keeps them
+        // streams past CH KiB (tier 1: 1,025 .. SLOT - 24 B, values snappy could not shrink, ~1
+        // in 3,000 dict values): the rest loaded here, synchronously -- rare, and it keeps them
         // out of the global-memory pass
-        for (uint64_t lm = __ballot(cur.mode == SL_LDS && cur.clen > 1024u); lm; lm &= lm - 1) {
+        for (uint64_t lm = __ballot(cur.mode == SL_LDS && cur.clen > 1024u * CH); lm; lm &= lm - 1) {
             const int b = __builtin_ctzll(lm);
             const uint32_t clb = __builtin_amdgcn_readlane(cur.clen, b);
-            if (1024u + 16 * lane < clb) {
-                const u32x4 c = ld16_hi(readlane_u64(cur.cp, b) + 1024u + 16 * lane, end);
-                *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + 1024u + 16 * lane) = c;
+            for (uint32_t off = 1024u * CH + 16 * lane; off < clb; off += 1024u) {
+                const u32x4 c = ld16_hi(readlane_u64(cur.cp, b) + off, end);
+                *reinterpret_cast<u32x4_lds_u *>(lds + b * SLOT + sl_pos<SLOT>(clb) + off) = c;
             }
         }
         sl_wsync();
-        // 2. descriptors of the group after next, then the next group's streams in flight
-        const SlRaw nn = load(g + 2 * G);
+        // 2. descriptors of the group after next (and the list entries of the one after
+        // that), then the next group's streams in flight
+        const SlRaw nn = load(ix2);
+        ix2 = index(g + 3 * G);
         prefetch(nxt);
         // 3. decode
         uint32_t fin = cur.status, mode = cur.mode;
@@ -479,21 +519,23 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
 #pragma unroll
             for (int b = 0; b < BPW; b++) {
                 const uint32_t dlb = __builtin_amdgcn_readlane(dl, b);
-                if (16 * lane < dlb) {
-                    const uint64_t ob = (uint64_t)out_vals + readlane_u64(cur.o0, b);
-                    st16_clip(ob + 16 * lane, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + 16 * lane),
-                              ob + dlb);
+                const uint64_t ob = (uint64_t)out_vals + readlane_u64(cur.o0, b);
+#pragma unroll
+                for (uint32_t c = 0; c < DCH; c++) {
+                    const uint32_t off = 1024u * c + 16u * lane;
+                    if (off < dlb)
+                        st16_clip(ob + off, *reinterpret_cast<const u32x4_lds_u *>(lds + b * SLOT + off), ob + dlb);
                 }
             }
         }
         sl_wsync();
-        // 5. descriptors (SL_GLOBAL blocks stay provisional, listed for the k_snappy_rt pass)
+        // 5. descriptors (SL_GLOBAL blocks stay provisional, listed for the next tier)
         if (mode == SL_GLOBAL) {
-            const uint32_t k = atomicAdd(list, 1u);
-            list[1 + k] = g * BPW + lane;
+            const uint32_t k = atomicAdd(out_cnt, 1u);
+            out_ent[k] = cur.i;
         }
         if (mode == SL_LDS || mode == SL_TOOLARGE) {
-            uint32_t *dw = reinterpret_cast<uint32_t *>(out + g * BPW + lane);
+            uint32_t *dw = reinterpret_cast<uint32_t *>(out + cur.i);
             dw[2] = 0;
             dw[3] = (fin == BHG_ST_OK || fin == BHG_ST_CRC_MISMATCH) ? cur.dlen : 0u;
             dw[9] = fin;
@@ -503,26 +545,40 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     }
 }
 
+template <int BPW, int SLOT, int CH, bool LISTED>
+static hipError_t launch_snappy_tier(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h,
+                                     uint32_t n, bhg_desc *out, uint8_t *out_vals, uint64_t out_cap,
+                                     const uint64_t *val_off, const uint32_t *in_cnt, const uint32_t *in_ent,
+                                     uint32_t *out_cnt, uint32_t *out_ent) {
+    // resident workgroups per CU (LDS-bound); a grid past that would start its extra
+    // workgroups only when the first ones finish
+    static const uint32_t per_cu =
+        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, LISTED>, 64, (160u * 1024u) / (BPW * SLOT + 64));
+    const uint32_t groups = (n + BPW - 1) / BPW;
+    const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
+    uint32_t grid = groups < cap ? groups : cap;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, LISTED>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+                       out_vals, out_cap, val_off, in_cnt, in_ent, out_cnt, out_ent);
+    return hipGetLastError();
+}
+
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list) {
     if (src_len >= 64 && list) {
-        if (hipError_t e = hipMemsetAsync(list, 0, 4, L.stream)) return e;
-        constexpr uint32_t BPW = kSlBpw, SLOT = kSlSlot;
-        // resident workgroups per CU (LDS-bound: 8 at 18 x 1,088 B); a grid past that would
-        // start its extra workgroups only when the first ones finish
-        static const uint32_t per_cu =
-            resident_per_cu((const void *)k_snappy_lds<BPW, SLOT>, 64, (160u * 1024u) / (BPW * SLOT + 64));
-        const uint32_t groups = (n + BPW - 1) / BPW;
-        const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
-        uint32_t grid = groups < cap ? groups : cap;
-        if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                           out_vals, out_cap, val_off, list);
-        if (hipError_t e = hipGetLastError()) return e;
-        // then the blocks it listed (too big for a slot), lane per block from global memory
+        // list layout (snappy_list_bytes): the two counts, tier 1's list, tier 2's list
+        uint32_t *c1 = list, *c2 = list + 1, *e1 = list + 2, *e2 = list + 2 + n;
+        if (hipError_t e = hipMemsetAsync(list, 0, 8, L.stream)) return e;
+        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, false>(L, src, src_len, h, n, out, out_vals, out_cap,
+                                                                         val_off, nullptr, nullptr, c1, e1))
+            return e;
+        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, true>(L, src, src_len, h, n, out, out_vals,
+                                                                              out_cap, val_off, c1, e1, c2, e2))
+            return e;
+        // then the blocks tier 2 listed (too big for a slot), lane per block from global memory
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
-                           out_cap, val_off, (const uint32_t *)list);
+                           out_cap, val_off, (const uint32_t *)c2, (const uint32_t *)e2);
         return hipGetLastError();
     }
     uint32_t grid = (n + 255) / 256;
@@ -530,7 +586,7 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(k_snappy_rt, dim3(grid), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals, out_cap,
-                       val_off, (const uint32_t *)nullptr);
+                       val_off, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 

@@ -87,12 +87,17 @@ def test_shipped_library_has_default_knobs():
     nch = _src_default("bhg_decode_tile.hip", "kTileNch")
     bpw = _src_default("bhg_snappy_dec.hip", "kSlBpw")
     slot = _src_default("bhg_snappy_dec.hip", "kSlSlot")
+    bpw2 = _src_default("bhg_snappy_dec.hip", "kSlBpw2")
+    slot2 = _src_default("bhg_snappy_dec.hip", "kSlSlot2")
+    ch2 = _src_default("bhg_snappy_dec.hip", "kSlCh2")
     want = {
-        rb"_ZN3bhg13k_decode_tileI": b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf),
-        rb"_ZN3bhg12k_snappy_ldsI": b"_ZN3bhg12k_snappy_ldsILi%dELi%dEE" % (bpw, slot),
+        rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf)},
+        # the two LDS tiers: every block (1-KiB slots), then the blocks tier 1 lists (4-KiB slots)
+        rb"_ZN3bhg12k_snappy_ldsI": {b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELb0EE" % (bpw, slot),
+                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi%dELb1EE" % (bpw2, slot2, ch2)},
     }
-    for prefix, name in want.items():
+    for prefix, names in want.items():
         found = set(re.findall(re.escape(prefix) + rb"[A-Za-z0-9]+?EE", blob))
-        assert found == {name}, (prefix, found, name)
+        assert found == names, (prefix, found, names)
     enc = set(re.findall(rb"_ZN3bhg12k_snappy_encI[A-Za-z0-9]+?EE", blob))
     assert enc == {b"_ZN3bhg12k_snappy_encILi2048ELi1ELi4EE", b"_ZN3bhg12k_snappy_encILi4096ELi3ELi3EE"}, enc

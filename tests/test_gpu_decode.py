@@ -283,6 +283,57 @@ def test_snappy_long_streams_in_lds(codec):
     assert gvals.tobytes() == evals[:int(eoff[-1])].tobytes()
 
 
+def test_snappy_tier2_slots(codec):
+    """Values decoding to 1-4 KiB go to the second LDS tier (4,160-B slots, 4 stream
+    chunks per lane): ordinary 1,025..4,096-B blocks, tier-1 spill hand-overs, streams past
+    4 KiB (incompressible 4,000..4,096-B values: the tail loaded at the dump), a tier-2
+    in-place spill (2,800 B of RLE copies, then 1,296 one-byte copies) and corrupt
+    1-4 KiB streams, mixed with > 4 KiB blocks for the global-memory pass.  The last
+    record (the end of src) is a tier-2 stream past 4 KiB."""
+    rng = random.Random(44)
+    body = bytes([0 << 2]) + b"x"
+    body += (bytes([(64 - 1) << 2 | 2]) + (1).to_bytes(2, "little")) * 43   # 2,753 B
+    body += bytes([(47 - 1) << 2 | 2]) + (1).to_bytes(2, "little")          # 2,800 B
+    body += (bytes([0 << 2 | 2]) + (7).to_bytes(2, "little")) * 1296       # 4,096 B
+    spill2 = _uvarint(4096) + body
+    assert O.snappy_decode(spill2) is not None and len(spill2) + 24 <= 4160
+    streams = []
+    for i in range(2400):
+        k = i % 10
+        if k == 0:
+            streams.append(spill2)
+        elif k == 1:
+            streams.append(O.snappy_encode(rand_bytes(rng, rng.choice([4000, 4070, 4096]))))
+        elif k == 2:
+            good = O.snappy_encode(compressible(rng, rng.choice([1500, 4096])))
+            streams.append(good[:-rng.randrange(1, 6)] if i % 20 == 2 else good[:5] + b"\x01\xff" + good[7:])
+        elif k == 3:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([4097, 6000]))))
+        elif k == 4:
+            streams.append(O.snappy_encode(rand_bytes(rng, 1024)))
+        else:
+            streams.append(O.snappy_encode(compressible(rng, rng.randrange(1025, 4097))))
+    streams.append(O.snappy_encode(rand_bytes(rng, 4096)))
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"t2-%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    # a corrupt block's slot holds no value (the reference returns snappy.ErrCorrupt): ok blocks only
+    bad = [(i, int(eoff[i + 1] - eoff[i]), len(streams[i])) for i in range(len(streams))
+           if exp["status"][i] == 0 and gvals[int(goff[i]):int(goff[i + 1])].tobytes() != evals[int(eoff[i]):int(eoff[i + 1])].tobytes()]
+    assert not bad, "blocks differ (index, dlen, clen): %s of %d" % (bad[:12], len(bad))
+    st = exp["status"]
+    assert (st[0::10] == 0).all() and (st[1::10] == 0).all() and (st[5::10] == 0).all()
+    assert (st[2::10] == O.SNAPPY_CORRUPT).sum() > 100
+
+
 def _view_with_bit31(nbytes, dev):
     """A uint8 device view of nbytes whose address has bit 31 of its low word set
     over its whole length (low word in [0x80000100, 0xFFFFFFFF])."""

@@ -20,7 +20,8 @@ from oracle import oracle as O
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "bitalosdb_amd", "csrc", "bhg_snappy_dec.hip")
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
-SLOT = 1088  # kSlSlot (bhg_snappy_dec.hip)
+SLOT = 1088   # kSlSlot (bhg_snappy_dec.hip): tier 1, values <= 1 KiB
+SLOT2 = 4160  # kSlSlot2: tier 2, values <= 4 KiB
 
 
 @pytest.fixture(scope="module")
@@ -29,7 +30,7 @@ def walk(tmp_path_factory):
         pytest.skip("no clang++")
     s = open(SRC).read()
     i0 = s.index("__device__ __forceinline__ uint32_t snappy_walk_lds(")
-    i1 = s.index("}  // namespace\n\ntemplate <int BPW")
+    i1 = s.index("\n}\n", i0) + 3  # the end of the function
     body = s[i0:i1].replace("__device__ __forceinline__ ", 'extern "C" ')
     hdr = ("#include <stdint.h>\n"
            "#define __builtin_amdgcn_s_waitcnt(x) ((void)0)\n"   # a wait-count hint on the GPU
@@ -46,11 +47,11 @@ def walk(tmp_path_factory):
     return lib
 
 
-def run_slot(walk, stream, dlen):
+def run_slot(walk, stream, dlen, slot=SLOT):
     """Stage `stream` as k_snappy_lds does and walk it; returns (code, output bytes)."""
     clen = len(stream)
-    pos = (SLOT - 8 - ((clen + 15) & ~15)) & ~15
-    lds = np.zeros(2 * SLOT + 64, dtype=np.uint8)   # the slot, then a neighbour slot and the pad
+    pos = (slot - 8 - ((clen + 15) & ~15)) & ~15
+    lds = np.zeros(2 * slot + 64, dtype=np.uint8)   # the slot, then a neighbour slot and the pad
     lds[pos:pos + clen] = np.frombuffer(stream, dtype=np.uint8)
     hdr = 0
     while hdr < 5 and lds[pos + hdr] >= 0x80:
@@ -98,6 +99,37 @@ def test_walk_matches_restated_decode(walk):
         if r == 0:
             assert out == v
     assert codes[0] > 1000
+
+
+def test_walk_tier2_slots(walk):
+    """The same walk in tier 2's 4,160-B slots: values of 1-4 KiB (dict-like tokens, runs,
+    incompressible) decode to the restated bytes or are handed over, never wrong."""
+    rng = random.Random(9)
+    dic = bytes(rng.getrandbits(8) for _ in range(4096))
+    codes = {0: 0, 1: 0, 2: 0}
+    for i in range(300):
+        n = rng.choice([1025, 1500, 2048, 3000, 4000, 4096])
+        k = i % 3
+        if k == 0:
+            v = bytearray()
+            while len(v) < n:
+                a = rng.randrange(0, 4000)
+                v += dic[a:a + rng.randrange(4, 65)] if rng.random() > 0.2 else bytes(
+                    rng.getrandbits(8) for _ in range(rng.randrange(4, 65)))
+            v = bytes(v[:n])
+        elif k == 1:
+            v = bytes(rng.getrandbits(8) for _ in range(n))
+        else:
+            v = (b"abc" * 2000)[:n]
+        st = O.snappy_encode(v)
+        if len(st) + 24 > SLOT2:
+            continue
+        r, out = run_slot(walk, st, len(v), SLOT2)
+        codes[r] += 1
+        assert r != 1
+        if r == 0:
+            assert out == v
+    assert codes[0] > 250
 
 
 def test_walk_hands_over_when_output_overtakes_stream(walk):
