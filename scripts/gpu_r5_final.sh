@@ -2,6 +2,7 @@
 # round 5 closing measurements on the committed tree, in two parts (one gpurun call each):
 #   PART=a: GPU tests, smoke, the driver-shaped C2 line, C2 kernel stats, C2 SQ counters
 #   PART=b: C3 / C4 / C5-snappy / mixdec / Get / tail / indexcrc lines, kernel stats, C3 + C4 SQ counters, gloo x2
+#   PART=c: part b from the tail line on
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -15,7 +16,7 @@ stats() {  # stats <name> <bench args...>: rocprofv3 kernel stats of one bench l
 line() {  # line <name> <bench args...>
   local nm=$1; shift
   timeout -k 10 500 python3 -u bench.py "$@" > $O/bench_$nm.json 2> $O/bench_$nm.err || { tail -20 $O/bench_$nm.err; return 1; }
-  python3 -c "import json; d=json.load(open('$O/bench_$nm.json')); print('$nm', d['value'], d['unit'], d['ms_per_step'], d['roofline']['frac'])"
+  python3 -c "import json; d=json.load(open('$O/bench_$nm.json')); print('$nm', d['value'], d['unit'], d.get('ms_per_step'), d.get('roofline', {}).get('frac'))"
 }
 if [ "$PART" = a ]; then
   timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
@@ -26,6 +27,7 @@ if [ "$PART" = a ]; then
   stats c2 --warmup 5 --no-cpu --no-e2e --no-traffic --no-c5 &&
   ARGS="--warmup 5" TAG=final/pmc_c2 KERNEL=k_decode_tile bash scripts/pmc_bench.sh
 else
+  [ "$PART" = c ] || {
   line c3 --config c3 --warmup 5 &&
   stats c3 --config c3 --warmup 5 --no-cpu --no-e2e --no-secondary &&
   line c4 --config c4 --warmup 5 &&
@@ -33,7 +35,7 @@ else
   line c5_snappy --config c5 --codec snappy --warmup 2 &&
   line mixdec --config mixdec --steps 10 --warmup 5 &&
   stats mixdec --config mixdec --steps 10 --warmup 5 &&
-  line get --config get --warmup 5 &&
+  line get --config get --warmup 5; } &&
   line tail --config tail --warmup 5 &&
   line indexcrc --config indexcrc --warmup 5 &&
   line g2_gloo --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu --no-e2e --no-c5 &&
