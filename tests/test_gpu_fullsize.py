@@ -103,3 +103,57 @@ def test_full_size_c4_parity(codec, gen):
     total = int(bufs.summary[0].item())
     assert total == len(exp["out"]) and total > 1 << 29
     assert out[:total].cpu().numpy().tobytes() == exp["out"].tobytes()
+
+
+@pytest.mark.parametrize("compressor", [0, 1])
+def test_full_size_mixed_decode_parity(codec, compressor):
+    """The C4-shaped tables decoded (bench.py --config mixdec): 1M pairs with values U[64, 4096] B
+    of the dict generator, GPU-encoded with either codec into 128 MiB tables, then the whole batch
+    decoded with the writer's CRCs.  Every descriptor and every decoded byte against the C
+    restatement, and every value against the encoder's input -- for snappy that runs both LDS
+    tiers (76 % of the blocks decode to more than 1 KiB) and leaves k_snappy_rt nothing."""
+    from bitalosdb_amd.codec import handles_tensor
+    n = 1_000_000
+    g = torch.Generator().manual_seed(0xD4)
+    val_lens = torch.randint(64, 4097, (n,), generator=g, dtype=torch.int64)
+    (keys, _, _, vals, val_off), out, bufs = _encode(codec, n, val_lens, 0xD4, compressor)
+    total = int(bufs.summary[0].item())
+    assert int(bufs.summary[2].item()) == 0 and total > 1 << 29
+    h = np.zeros(n, dtype=O.HANDLE_DT)
+    h["offset"] = bufs.pos.cpu().numpy().view(np.uint64)
+    h["length"] = bufs.bh_len.cpu().numpy().view(np.uint32)
+    exp_crc = bufs.crc.cpu().numpy().view(np.uint32)
+    dev = codec.device
+    with torch.cuda.stream(codec.stream):
+        src = out[:total]
+        ht = handles_tensor(h, dev)
+        ec = bufs.crc
+        if compressor == 1:
+            probe = codec.decode_batch(src, total, ht, n, 1, expected_crc=ec)
+            codec.sync()
+            tot = int(probe.val_off_np()[-1])
+            assert tot == int(val_off[-1].item())
+            dv = torch.empty(tot, dtype=torch.uint8, device=dev)
+            res = codec.decode_batch(src, total, ht, n, 1, expected_crc=ec, out_vals=dv)
+        else:
+            res = codec.decode_batch(src, total, ht, n, 0, expected_crc=ec)
+        codec.sync()
+    got = res.desc_np()
+    assert (got["status"] == 0).all()
+    host = src.cpu().numpy()
+    exp, ev, eo = O.decode_batch(host, h, codec=compressor, expected_crc=exp_crc, nthreads=16)
+    for f in exp.dtype.names:
+        bad = np.nonzero(got[f] != exp[f])[0]
+        assert bad.size == 0, (f, bad[:8])
+    vin = vals.cpu().numpy()
+    if compressor == 1:
+        gv = dv.cpu().numpy()
+        assert np.array_equal(res.val_off_np(), eo)
+        assert gv.tobytes() == ev[:tot].tobytes()
+        assert gv.tobytes() == vin.tobytes()                       # round trip to the encoder's input
+    else:
+        # NoCompressor values are views into src: gather them and compare with the input
+        vo = got["val_off"].astype(np.int64) + h["offset"].astype(np.int64)
+        vl = got["val_len"].astype(np.int64)
+        assert np.array_equal(vl, np.diff(val_off.cpu().numpy()))
+        assert np.concatenate([host[a:a + b] for a, b in zip(vo.tolist(), vl.tolist())]).tobytes() == vin.tobytes()
