@@ -386,16 +386,19 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (codec == BHG_CODEC_SNAPPY && !out_val_off) { set_err(c, "snappy decode needs out_val_off[n+1]"); return BHG_EINVAL; }
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
-    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
-    if (codec == BHG_CODEC_SNAPPY) {
-        Scratch sc;
-        const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
-        if (int r = scratch_alloc(c, L.stream, scan_b + (out_vals ? bhg::snappy_list_bytes(n) : 0), sc)) return r;
-        HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
-        if (out_vals)
-            HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off,
-                                          reinterpret_cast<uint32_t *>(sc.base + scan_b)));
+    if (codec != BHG_CODEC_SNAPPY) {
+        HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
+        return BHG_OK;
     }
+    // snappy: the header pass also sorts the blocks into the decode lists (when values are wanted)
+    Scratch sc;
+    const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
+    if (int r = scratch_alloc(c, L.stream, scan_b + (out_vals ? bhg::snappy_list_bytes(n) : 0), sc)) return r;
+    uint32_t *lists = out_vals ? reinterpret_cast<uint32_t *>(sc.base + scan_b) : nullptr;
+    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off, lists));
+    HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
+    if (out_vals)
+        HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off, lists));
     return BHG_OK;
 }
 
@@ -637,7 +640,7 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
         HIP_TRY(c, hipMemcpyAsync(S.h, handles + ch.a, (size_t)ch.cn * sizeof(bhg_handle), hipMemcpyHostToDevice, sc));
         if (S.e) HIP_TRY(c, hipMemcpyAsync(S.e, expected_crc + ch.a, (size_t)ch.cn * 4, hipMemcpyHostToDevice, sc));
         HIP_TRY(c, bhg::launch_add_u64(L, reinterpret_cast<uint64_t *>(S.h), ch.cn, 0 - ch.lo, 2));
-        HIP_TRY(c, bhg::launch_decode(L, S.src, ch.hi - ch.lo, S.h, ch.cn, BHG_CODEC_SNAPPY, S.e, S.d, S.off));
+        HIP_TRY(c, bhg::launch_decode(L, S.src, ch.hi - ch.lo, S.h, ch.cn, BHG_CODEC_SNAPPY, S.e, S.d, S.off, S.list));
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, S.off, S.off, ch.cn, S.scan));
         HIP_TRY(c, hipMemcpyAsync(c->ptot + ch.slot, S.off + ch.cn, 8, hipMemcpyDeviceToHost, sc));
         HIP_TRY(c, hipEventRecord(c->pev[ch.slot], sc));
@@ -860,7 +863,8 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
     if (de) HIP_TRY(c, hipMemcpyAsync(de, expected_crc, eb, hipMemcpyHostToDevice, s));
     bhg::Launch L = launch_of(c, nullptr);
     const uint8_t *dsrc = reinterpret_cast<const uint8_t *>(c->h_src);
-    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, codec, de, dd, doff));
+    HIP_TRY(c, bhg::launch_decode(L, dsrc, src_len, dh, n, codec, de, dd, doff,
+                                  codec == BHG_CODEC_SNAPPY && out_vals ? dlist : nullptr));
     if (codec == BHG_CODEC_SNAPPY) {
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, doff, doff, n, dscan));
         HIP_TRY(c, hipMemcpyAsync(out_val_off, doff, ob, hipMemcpyDeviceToHost, s));

@@ -34,6 +34,7 @@
 #pragma once
 #include "bhg_crc_tables.h"
 #include "bhg_device.h"
+#include "bhg_internal.h"
 
 namespace bhg {
 
@@ -86,7 +87,8 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                                                             const bhg_handle *__restrict__ handles, uint32_t n,
                                                             const uint32_t *__restrict__ expected_crc,
                                                             bhg_desc *__restrict__ out, uint64_t *__restrict__ sizes,
-                                                            const uint32_t *__restrict__ gtab) {
+                                                            const uint32_t *__restrict__ gtab,
+                                                            uint32_t *__restrict__ lists, uint32_t sub_cap) {
     using namespace stream_detail;
     static_assert(WIN == 128 || WIN == 256, "128- or 256-byte windows");
     constexpr int NW = WIN / 4;   // words per window
@@ -394,10 +396,12 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             if (rcrc == 0x9e3779b9u) out[i].crc = rcrc;
             continue;
         }
+        bool to_small = false, to_large = false;  // MODE 1: the decode list this lane's block joins
         if (valid) {
             // ---- readRecordHeader / readRecord / readKV from the record's first 60 bytes
             uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
             uint64_t dtr = 0, dsize = 0;
+            uint32_t vlen = 0;  // MODE 1: the stored (compressed) value length
             if (inb) {
                 const uint32_t hsh = (uint32_t)(p & 3);
                 uint32_t rw[15];
@@ -476,6 +480,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                             dsize = x;
                             dvl = (uint32_t)x;  // provisional: the snappy kernel finalises
                             dvo = 12 + k;       // provisional: compressed payload offset
+                            vlen = v;
                         }
                     }
                     if (expected_crc != nullptr && dst == BHG_ST_OK && ecrc != dcrc) dst = BHG_ST_CRC_MISMATCH;
@@ -494,6 +499,30 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             o[3] = make_uint2(dfn, dfnv);
             o[4] = make_uint2(dcrc, dst);
             if (MODE == 1) sizes[i] = dsize;
+            if (MODE == 1 && (dst == BHG_ST_OK || dst == BHG_ST_CRC_MISMATCH)) {
+                // the block's decode list: the 1-KiB LDS slots (a value of <= 1 KiB whose stream fits
+                // beside it), else the 4-KiB tier (appended below, with the wave converged)
+                const bool small = dsize <= kSnapSmallMax && vlen + 24u <= kSnapSmallSlot;
+                to_small = small;
+                to_large = !small;
+            }
+        }
+        if (MODE == 1 && lists != nullptr) {
+            // one atomic per wave and list on sub-list (tile mod 64), then each lane's rank among
+            // the wave's blocks of that list (per-lane atomics on the 64 counters: C3 5.5 ms)
+            const uint32_t sub = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile) & 63u;
+            const uint64_t ms = __ballot(to_small), ml = __ballot(to_large);
+            uint32_t bs = 0, bl = 0;
+            if (lane == 0) {
+                if (ms) bs = atomicAdd(lists + sub, (uint32_t)__builtin_popcountll(ms));
+                if (ml) bl = atomicAdd(lists + 64 + sub, (uint32_t)__builtin_popcountll(ml));
+            }
+            bs = (uint32_t)__builtin_amdgcn_readfirstlane((int)bs);
+            bl = (uint32_t)__builtin_amdgcn_readfirstlane((int)bl);
+            const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            if (to_small) lists[kSnapListHdr + sub * sub_cap + bs + (uint32_t)__builtin_popcountll(ms & below)] = i;
+            if (to_large)
+                lists[kSnapListHdr + (64 + sub) * sub_cap + bl + (uint32_t)__builtin_popcountll(ml & below)] = i;
         }
     }
 }

@@ -15,7 +15,8 @@ void build_stream_tab_default(uint32_t *out) { build_stream_tab(out, kStreamWin,
 // MODE 1 only: the NoCompressor decode is k_decode_tile (MODE 0 of this kernel measured
 // slower, DESIGN.md 4.1, and stays a lab build)
 hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes) {
+                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
+                                uint32_t *lists) {
     if (mode != 1) return hipErrorInvalidValue;
     constexpr int WPB = 8;  // 156.5 KiB of LDS: one workgroup per CU
     const uint64_t tiles = (n + 63) / 64;
@@ -23,7 +24,8 @@ hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t sr
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL((k_decode_stream<1, kStreamNch, WPB, kStreamWin, kStreamPipe>), dim3(grid),
-                       dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab);
+                       dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab, lists,
+                       (uint32_t)snappy_sub_cap(n));
     return hipGetLastError();
 }
 

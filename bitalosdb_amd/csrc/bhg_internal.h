@@ -47,8 +47,11 @@ inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback
 
 // bhg_decode.hip: descriptors for codec NONE (complete) or the snappy header
 // pass (sizes[i] = decoded length; the values follow with launch_snappy)
+// lists: null, or (snappy) the decode lists of snappy_list_bytes(n) -- the header pass sorts the
+// blocks to decode into them by size for launch_snappy (which must get the same pointer)
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
+                         uint32_t *lists = nullptr);
 // bhg_decode_tile.hip: the NoCompressor decode kernel
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out);
@@ -57,15 +60,25 @@ hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_
 size_t stream_tab_words();
 void build_stream_tab_default(uint32_t *out);
 hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes);
+                                int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
+                                uint32_t *lists);
 // bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
-// list: device scratch of snappy_list_bytes(n) (the blocks each LDS tier hands to the
-// next: 1-KiB slots -> 4-KiB slots -> global memory); null -> every block through the
-// global-memory kernel
+// list: the decode lists the header pass filled (launch_decode with the same pointer, of
+// snappy_list_bytes(n)): the blocks for the 1-KiB LDS slots, those for the 4-KiB slots, and the
+// ones left for the global-memory pass; null -> every block through the global-memory kernel.
+// Layout (u32 words): [0, 64) small sub-list sizes, [64, 128) large sub-list sizes, [128] the
+// global-memory list's size; from kSnapListHdr: 64 small sub-lists of snappy_sub_cap(n) entries,
+// 64 large ones, then the global-memory list (n).  A header-pass tile t (64 handles) appends to
+// sub-list t mod 64, so no sub-list takes more than snappy_sub_cap(n) and the appends of ~16k
+// tiles spread over 64 counters.
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list);
-inline size_t snappy_list_bytes(uint32_t n) { return 8 + 8 * (size_t)n; }
+constexpr uint32_t kSnapListHdr = 256;
+constexpr uint32_t kSnapSmallMax = 1024;   // decoded bytes a tier-1 slot takes ...
+constexpr uint32_t kSnapSmallSlot = 1088;  // ... and its slot (the stream + 24 must fit too)
+inline size_t snappy_sub_cap(uint32_t n) { return 64 * (((size_t)n + 64 * 64 - 1) / (64 * 64)); }
+inline size_t snappy_list_bytes(uint32_t n) { return 4 * (kSnapListHdr + 128 * snappy_sub_cap(n) + (size_t)n); }
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)

@@ -391,49 +391,78 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 
 }  // namespace
 
-// Two tiers of the same kernel: <18, 1,088, 1> takes every block (values that
-// decode to <= 1 KiB), <6, 4,160, 2> the blocks tier 1 listed (values up to
-// 4 KiB, and tier-1 spills), and k_snappy_rt the rest.  in_cnt/in_ent
-// (LISTED false: every block) or the list to take; out_cnt/out_ent: where
-// blocks that do not fit are listed.  CH: 16-B stream chunks per lane per
-// block prefetched into VGPRs (the rest of a longer stream is loaded at the
-// dump).
-// Measured on the C4-shaped decode (bench.py --config mixdec: 1M values
-// U[64, 4096], 76 % of them > 1 KiB): the > 1 KiB blocks took 5.83 ms per
-// step in k_snappy_rt; tier 2 takes 4.2 ms (step 6.90 -> 5.27 ms, 137 -> 180
-// GiB/s).  Tier-2 shapes A/B'd (2 runs each, one box; profiles/r5/snappy_t2):
-// 6 blocks x 2 chunks 5.27 ms, 4 x 4 5.44, 3 x 4 5.52, 2 x 4 5.77; 64-B ops
-// (4 reads in flight per element) 6.3 ms and C3 +12 %; a 2-KiB class of 12
-// (or 9, 16) blocks per wave for values <= 2 KiB 5.30-5.47 ms; one WAVE per
-// block (wave-uniform SALU decode, byte-per-lane copies) 7.3 ms for tier 2
-// alone -- 73 SALU instructions per element for one block, where a lane walk
-// spends ~80 VALU per element step for 6.
-template <int BPW, int SLOT, int CH, bool LISTED>
+// Two tiers of the same kernel: <18, 1,088, 1> takes the blocks that decode to <= 1 KiB,
+// <6, 4,160, 2> the others, each from the header pass's 64 sub-lists of its size class
+// (launch_decode; in_cnt: the 64 sub-list sizes, in_ent: sub-list 0, sub_cap entries apart), and
+// k_snappy_rt what neither holds (out_cnt / out_ent: the blocks a tier hands on).  CH: 16-B
+// stream chunks per lane per block prefetched into VGPRs (the rest of a longer stream is loaded
+// at the dump).
+// Measured on the C4-shaped decode (bench.py --config mixdec: 1M values U[64, 4096], 76 % of
+// them > 1 KiB): the > 1 KiB blocks took 5.83 ms per step in k_snappy_rt; tier 2 takes 4.2 ms
+// (step 6.90 -> 5.27 ms, 137 -> 180 GiB/s).  Tier-2 shapes A/B'd (2 runs each, one box;
+// profiles/r5/snappy_t2): 6 blocks x 2 chunks 5.27 ms, 4 x 4 5.44, 3 x 4 5.52, 2 x 4 5.77; 64-B ops
+// (4 reads in flight per element) 6.3 ms and C3 +12 %; a 2-KiB class of 12 (or 9, 16) blocks per
+// wave for values <= 2 KiB 5.30-5.47 ms; one WAVE per block (wave-uniform SALU decode,
+// byte-per-lane copies) 7.3 ms for tier 2 alone -- ~75 SALU instructions per element for one
+// block, where a lane walk spends ~80 VALU per element step for 6.  Until round 5 tier 1 walked
+// every block (those it could not hold idled their lanes: 0.71 ms of the mixdec step for 24 % of
+// the blocks); the header pass now sorts them.
+// ORDER: 0 the list (tier 2); 1 the list unless the batch is mostly this class, 2 the batch's
+// own order only when it is (tier 1: two launches, each returning at once when not its case, so
+// neither carries the other's code)
+template <int BPW, int SLOT, int CH, int ORDER>
 __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
                                                    uint64_t out_cap, const uint64_t *__restrict__ val_off,
                                                    const uint32_t *__restrict__ in_cnt,
-                                                   const uint32_t *__restrict__ in_ent, uint32_t *__restrict__ out_cnt,
-                                                   uint32_t *__restrict__ out_ent) {
+                                                   const uint32_t *__restrict__ in_ent, uint32_t sub_cap,
+                                                   uint32_t *__restrict__ out_cnt, uint32_t *__restrict__ out_ent) {
     static_assert(SLOT % 16 == 0, "16-B aligned slots");
     constexpr uint32_t DMAX = SLOT - 64;            // longest decoded block a slot takes
     constexpr uint32_t DCH = (DMAX + 1023) / 1024;  // 1-KiB rows of the store-out
     __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint32_t cnt = LISTED ? *in_cnt : n;
+    // the sub-lists as one list: lane k holds the inclusive / exclusive prefix of their sizes at k
+    const uint32_t sz = in_cnt[lane];
+    const uint32_t incl = wave_incl_add(sz), excl = incl - sz;
+    const uint32_t lcnt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // tier 1: when at least 7/8 of the batch is in this class, walk the batch in its own order
+    // instead (the blocks of the other class skipped): the list's lookups and its order cost the
+    // all-1-KiB C3 step 4 % (0.958 -> 0.998 ms); mixed sizes gain from the list
+    const bool mostly = (uint64_t)lcnt * 8 >= (uint64_t)n * 7;
+    if ((ORDER == 1 && mostly) || (ORDER == 2 && !mostly)) return;
+    constexpr bool natural = ORDER == 2;
+    const uint32_t cnt = natural ? n : lcnt;
     const uint32_t ngroups = (cnt + BPW - 1) / BPW;
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
-    // block index of this lane in group grp (n: none); listed: one load, issued a group before
-    // the descriptor loads that need it
+    auto rl = [](uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); };
+    // block index of this lane in group grp (n: none): list position j = grp * BPW + lane, found in
+    // its sub-list by a wave-uniform search for the group's first position and a walk over the
+    // (usually no) sub-list ends the group spans; one load, issued a group before the descriptor
+    // loads that need it
     auto index = [&](uint32_t grp) -> uint32_t {
-        const uint32_t j = grp * BPW + lane;
-        const bool ok = lane < BPW && grp < ngroups && j < cnt;
-        if (!LISTED) return ok ? j : n;
-        const uint32_t x = in_ent[ok ? j : 0u];  // cnt >= 1 here
+        const uint32_t j0 = grp * BPW, j = j0 + lane;
+        if (grp >= ngroups) return n;
+        const bool ok = lane < BPW && j < cnt;
+        if (natural) return ok ? j : n;
+        uint32_t sidx = 0;
+        for (uint32_t step = 32; step; step >>= 1)
+            if (rl(incl, sidx + step - 1) <= j0) sidx += step;
+        uint32_t sl = sidx, b0 = rl(excl, sidx);
+        const uint32_t jl = j0 + BPW - 1 < cnt - 1 ? j0 + BPW - 1 : cnt - 1;
+        for (uint32_t t = sidx; t < 63; t++) {
+            const uint32_t it = rl(incl, t);
+            if (it > jl) break;
+            if (j >= it) {
+                sl = t + 1;
+                b0 = it;
+            }
+        }
+        const uint32_t x = in_ent[(size_t)sl * sub_cap + (ok ? j - b0 : 0u)];
         return ok ? x : n;
     };
     auto load = [&](uint32_t i) -> SlRaw { return sl_load(i < n ? i : n, n, out, handles, val_off); };
@@ -456,9 +485,15 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             }
         }
     };
-    SlInfo cur = sl_finish<SLOT>(load(index(g)), n, base, out_cap);
+    // in natural order, a block this tier cannot hold belongs to the other class's list: skipped
+    auto finish = [&](const SlRaw &w) -> SlInfo {
+        SlInfo r = sl_finish<SLOT>(w, n, base, out_cap);
+        if (natural && r.mode == SL_GLOBAL) r.mode = SL_SKIP;
+        return r;
+    };
+    SlInfo cur = finish(load(index(g)));
     prefetch(cur);
-    SlInfo nxt = sl_finish<SLOT>(load(index(g + G)), n, base, out_cap);
+    SlInfo nxt = finish(load(index(g + G)));
     uint32_t ix2 = index(g + 2 * G);
     for (; g < ngroups; g += G) {
         // 1. this group's streams -> slots
@@ -541,25 +576,25 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
             dw[9] = fin;
         }
         cur = nxt;
-        nxt = sl_finish<SLOT>(nn, n, base, out_cap);
+        nxt = finish(nn);
     }
 }
 
-template <int BPW, int SLOT, int CH, bool LISTED>
+template <int BPW, int SLOT, int CH, int ORDER>
 static hipError_t launch_snappy_tier(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h,
                                      uint32_t n, bhg_desc *out, uint8_t *out_vals, uint64_t out_cap,
                                      const uint64_t *val_off, const uint32_t *in_cnt, const uint32_t *in_ent,
-                                     uint32_t *out_cnt, uint32_t *out_ent) {
+                                     uint32_t sub_cap, uint32_t *out_cnt, uint32_t *out_ent) {
     // resident workgroups per CU (LDS-bound); a grid past that would start its extra
     // workgroups only when the first ones finish
     static const uint32_t per_cu =
-        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, LISTED>, 64, (160u * 1024u) / (BPW * SLOT + 64));
+        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, ORDER>, 64, (160u * 1024u) / (BPW * SLOT + 64));
     const uint32_t groups = (n + BPW - 1) / BPW;
     const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
     uint32_t grid = groups < cap ? groups : cap;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, LISTED>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                       out_vals, out_cap, val_off, in_cnt, in_ent, out_cnt, out_ent);
+    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, ORDER>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+                       out_vals, out_cap, val_off, in_cnt, in_ent, sub_cap, out_cnt, out_ent);
     return hipGetLastError();
 }
 
@@ -567,18 +602,26 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list) {
     if (src_len >= 64 && list) {
-        // list layout (snappy_list_bytes): the two counts, tier 1's list, tier 2's list
-        uint32_t *c1 = list, *c2 = list + 1, *e1 = list + 2, *e2 = list + 2 + n;
-        if (hipError_t e = hipMemsetAsync(list, 0, 8, L.stream)) return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, false>(L, src, src_len, h, n, out, out_vals, out_cap,
-                                                                         val_off, nullptr, nullptr, c1, e1))
+        // the lists the header pass filled (launch_decode with the same pointer; layout in
+        // bhg_internal.h): the <= 1-KiB class, the 1-4 KiB class, and the global-memory list
+        const uint32_t cap = (uint32_t)snappy_sub_cap(n);
+        uint32_t *c_small = list, *c_large = list + 64, *c_rt = list + 128;
+        uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * cap,
+                 *e_rt = e_large + (size_t)64 * cap;
+        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 2>(L, src, src_len, h, n, out, out_vals, out_cap,
+                                                                     val_off, c_small, e_small, cap, c_rt, e_rt))
             return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, true>(L, src, src_len, h, n, out, out_vals,
-                                                                              out_cap, val_off, c1, e1, c2, e2))
+        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 1>(L, src, src_len, h, n, out, out_vals, out_cap,
+                                                                     val_off, c_small, e_small, cap, c_rt, e_rt))
             return e;
-        // then the blocks tier 2 listed (too big for a slot), lane per block from global memory
+        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, 0>(L, src, src_len, h, n, out, out_vals,
+                                                                         out_cap, val_off, c_large, e_large, cap,
+                                                                         c_rt, e_rt))
+            return e;
+        // then the blocks the tiers handed on (too big for a slot, or an in-place spill), lane per
+        // block from global memory
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
-                           out_cap, val_off, (const uint32_t *)c2, (const uint32_t *)e2);
+                           out_cap, val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt);
         return hipGetLastError();
     }
     uint32_t grid = (n + 255) / 256;

@@ -334,6 +334,43 @@ def test_snappy_tier2_slots(codec):
     assert (st[2::10] == O.SNAPPY_CORRUPT).sum() > 100
 
 
+def test_snappy_small_majority_with_large_minority(codec):
+    """Tier 1 walks the batch in its own order when >= 7/8 of the blocks are <= 1 KiB (and the
+    header pass's list otherwise): a batch of 1-KiB blocks with a minority of 1-4 KiB and
+    > 4 KiB blocks, spills and incompressible 1 KiB values, corrupt and oversize streams among
+    them -- the minority must be decoded by tier 2 / the global pass exactly once."""
+    rng = random.Random(55)
+    streams = []
+    for i in range(2400):
+        k = i % 40
+        if k == 0:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([1500, 3000, 4096]))))
+        elif k == 1:
+            streams.append(O.snappy_encode(compressible(rng, 9000)))
+        elif k == 2:
+            streams.append(O.snappy_encode(rand_bytes(rng, 1024)))        # stream > 1,064 B: the 4-KiB tier
+        elif k == 3:
+            good = O.snappy_encode(compressible(rng, 1024))
+            streams.append(good[:-2])                                    # corrupt
+        else:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([16, 500, 1000, 1024]))))
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"nat-%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    ok = [i for i in range(len(streams)) if exp["status"][i] == 0]
+    assert len(ok) >= 2300
+    for i in ok:
+        assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
+
+
 def _view_with_bit31(nbytes, dev):
     """A uint8 device view of nbytes whose address has bit 31 of its low word set
     over its whole length (low word in [0x80000100, 0xFFFFFFFF])."""
