@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             if (rcrc == 0x9e3779b9u) out[i].crc = rcrc;
             continue;
         }
-        bool to_small = false, to_large = false;  // MODE 1: the decode list this lane's block joins
+        uint32_t cls = ~0u;  // MODE 1: the decode list this lane's block joins (0 small, 1.. large buckets)
         if (valid) {
             // ---- readRecordHeader / readRecord / readKV from the record's first 60 bytes
             uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
@@ -501,28 +501,37 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             if (MODE == 1) sizes[i] = dsize;
             if (MODE == 1 && (dst == BHG_ST_OK || dst == BHG_ST_CRC_MISMATCH)) {
                 // the block's decode list: the 1-KiB LDS slots (a value of <= 1 KiB whose stream fits
-                // beside it), else the 4-KiB tier (appended below, with the wave converged)
+                // beside it), else the 4-KiB tier's bucket of its decoded size, largest first
+                // (appended below, with the wave converged)
                 const bool small = dsize <= kSnapSmallMax && vlen + 24u <= kSnapSmallSlot;
-                to_small = small;
-                to_large = !small;
+                const uint32_t b = dsize <= kSnapSmallMax ? 0u : (uint32_t)((dsize - kSnapSmallMax - 1) / kSnapBucketBytes);
+                cls = small ? 0u : 1u + (kSnapBuckets - 1) - (b < kSnapBuckets - 1 ? b : kSnapBuckets - 1);
             }
         }
         if (MODE == 1 && lists != nullptr) {
-            // one atomic per wave and list on sub-list (tile mod 64), then each lane's rank among
-            // the wave's blocks of that list (per-lane atomics on the 64 counters: C3 5.5 ms)
+            // one atomic per wave and list on sub-list (tile mod 64) of each class present, all
+            // issued before any result is used, then each lane's rank among the wave's blocks of
+            // its class (per-lane atomics on the counters: C3 5.5 ms)
             const uint32_t sub = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile) & 63u;
-            const uint64_t ms = __ballot(to_small), ml = __ballot(to_large);
-            uint32_t bs = 0, bl = 0;
-            if (lane == 0) {
-                if (ms) bs = atomicAdd(lists + sub, (uint32_t)__builtin_popcountll(ms));
-                if (ml) bl = atomicAdd(lists + 64 + sub, (uint32_t)__builtin_popcountll(ml));
-            }
-            bs = (uint32_t)__builtin_amdgcn_readfirstlane((int)bs);
-            bl = (uint32_t)__builtin_amdgcn_readfirstlane((int)bl);
             const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            if (to_small) lists[kSnapListHdr + sub * sub_cap + bs + (uint32_t)__builtin_popcountll(ms & below)] = i;
-            if (to_large)
-                lists[kSnapListHdr + (64 + sub) * sub_cap + bl + (uint32_t)__builtin_popcountll(ml & below)] = i;
+            uint64_t cm[1 + kSnapBuckets];
+            uint32_t cb[1 + kSnapBuckets];
+#pragma unroll
+            for (uint32_t q = 0; q <= kSnapBuckets; q++) {
+                cm[q] = __ballot(cls == q);
+                cb[q] = 0;
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (uint32_t q = 0; q <= kSnapBuckets; q++)
+                    if (cm[q]) cb[q] = atomicAdd(lists + 64 * q + sub, (uint32_t)__builtin_popcountll(cm[q]));
+            }
+#pragma unroll
+            for (uint32_t q = 0; q <= kSnapBuckets; q++) {
+                const uint32_t bq = (uint32_t)__builtin_amdgcn_readfirstlane((int)cb[q]);
+                if (cls == q)
+                    lists[kSnapListHdr + (64 * q + sub) * sub_cap + bq + (uint32_t)__builtin_popcountll(cm[q] & below)] = i;
+            }
         }
     }
 }

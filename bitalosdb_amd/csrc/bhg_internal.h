@@ -64,21 +64,28 @@ hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t sr
                                 uint32_t *lists);
 // bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
 // list: the decode lists the header pass filled (launch_decode with the same pointer, of
-// snappy_list_bytes(n)): the blocks for the 1-KiB LDS slots, those for the 4-KiB slots, and the
-// ones left for the global-memory pass; null -> every block through the global-memory kernel.
-// Layout (u32 words): [0, 64) small sub-list sizes, [64, 128) large sub-list sizes, [128] the
-// global-memory list's size; from kSnapListHdr: 64 small sub-lists of snappy_sub_cap(n) entries,
-// 64 large ones, then the global-memory list (n).  A header-pass tile t (64 handles) appends to
-// sub-list t mod 64, so no sub-list takes more than snappy_sub_cap(n) and the appends of ~16k
-// tiles spread over 64 counters.
+// snappy_list_bytes(n)): the blocks for the 1-KiB LDS slots, those for the 4-KiB slots in
+// kSnapBuckets buckets of decoded size, and the ones left for the global-memory pass; null ->
+// every block through the global-memory kernel.  Layout (u32 words): [0, 64) the small
+// sub-lists' sizes, [64, 64 + 64 kSnapBuckets) the large ones' (largest bucket first), then the
+// global-memory list's size; from kSnapListHdr the sub-lists themselves, snappy_sub_cap(n)
+// entries apart (small, then large in the same order), then the global-memory list (n).  A
+// header-pass tile t (64 handles) appends to sub-list t mod 64 of its class, so no sub-list takes
+// more than snappy_sub_cap(n) and the appends of ~16k tiles spread over 64 counters per class.
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list);
-constexpr uint32_t kSnapListHdr = 256;
+// size buckets of the 4-KiB tier, so a wave's 6 blocks walk alike (it runs as long as its longest):
+// mixdec 4.89 -> 4.28 ms with 4; 8 and 12 buckets 4.31-4.32 / 4.36-4.39 (profiles/r5/snappy_buckets)
+constexpr uint32_t kSnapBuckets = 4;
+constexpr uint32_t kSnapBucketBytes = 3072 / kSnapBuckets;  // decoded bytes per bucket above 1 KiB
+constexpr uint32_t kSnapSubs = 64 * (1 + kSnapBuckets);
+constexpr uint32_t kSnapRtCount = kSnapSubs;  // word of the global-memory list's size
+constexpr uint32_t kSnapListHdr = (kSnapSubs + 1 + 255) / 256 * 256;  // the sizes, rounded to 1 KiB
 constexpr uint32_t kSnapSmallMax = 1024;   // decoded bytes a tier-1 slot takes ...
 constexpr uint32_t kSnapSmallSlot = 1088;  // ... and its slot (the stream + 24 must fit too)
 inline size_t snappy_sub_cap(uint32_t n) { return 64 * (((size_t)n + 64 * 64 - 1) / (64 * 64)); }
-inline size_t snappy_list_bytes(uint32_t n) { return 4 * (kSnapListHdr + 128 * snappy_sub_cap(n) + (size_t)n); }
+inline size_t snappy_list_bytes(uint32_t n) { return 4 * (kSnapListHdr + (size_t)kSnapSubs * snappy_sub_cap(n) + (size_t)n); }
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                              uint32_t *out);
 // one workgroup per range (long ranges: the per-table indexhash checksum)

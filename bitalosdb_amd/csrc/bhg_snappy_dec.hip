@@ -406,11 +406,13 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 // byte-per-lane copies) 7.3 ms for tier 2 alone -- ~75 SALU instructions per element for one
 // block, where a lane walk spends ~80 VALU per element step for 6.  Until round 5 tier 1 walked
 // every block (those it could not hold idled their lanes: 0.71 ms of the mixdec step for 24 % of
-// the blocks); the header pass now sorts them.
+// the blocks); the header pass now sorts them (mixdec 5.27 -> 4.89 ms), tier 2's by decoded size
+// into 4 buckets so that a wave's 6 lanes finish together (4.89 -> 4.28 ms; the tier was issue
+// bound, ~195 instructions per wave element step with the walk as long as its longest block).
 // ORDER: 0 the list (tier 2); 1 the list unless the batch is mostly this class, 2 the batch's
 // own order only when it is (tier 1: two launches, each returning at once when not its case, so
 // neither carries the other's code)
-template <int BPW, int SLOT, int CH, int ORDER>
+template <int BPW, int SLOT, int CH, int ORDER, int NSUB>
 __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
                                                    const bhg_handle *__restrict__ handles, uint32_t n,
                                                    bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
@@ -425,9 +427,19 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
     // the sub-lists as one list: lane k holds the inclusive / exclusive prefix of their sizes at k
-    const uint32_t sz = in_cnt[lane];
-    const uint32_t incl = wave_incl_add(sz), excl = incl - sz;
-    const uint32_t lcnt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // NSUB sub-lists as one list: lane k of register r holds the inclusive / exclusive prefix of
+    // their sizes at sub-list 64 r + k
+    static_assert(NSUB % 64 == 0 && NSUB <= 1024, "sub-lists");
+    constexpr int NR = NSUB / 64;
+    uint32_t incl[NR], excl[NR];
+    uint32_t lcnt = 0;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const uint32_t sz = in_cnt[64 * r + lane];
+        incl[r] = wave_incl_add(sz) + lcnt;
+        excl[r] = incl[r] - sz;
+        lcnt = (uint32_t)__builtin_amdgcn_readlane((int)incl[r], 63);
+    }
     // tier 1: when at least 7/8 of the batch is in this class, walk the batch in its own order
     // instead (the blocks of the other class skipped): the list's lookups and its order cost the
     // all-1-KiB C3 step 4 % (0.958 -> 0.998 ms); mixed sizes gain from the list
@@ -439,7 +451,14 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     const uint32_t G = gridDim.x;
     uint32_t g = blockIdx.x;
     if (g >= ngroups) return;
-    auto rl = [](uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); };
+    // sub-list t's prefix (t wave-uniform)
+    auto rl = [](const uint32_t *v, uint32_t t) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int r = 0; r < NR; r++)
+            if ((t >> 6) == (uint32_t)r) x = (uint32_t)__builtin_amdgcn_readlane((int)v[r], (int)(t & 63u));
+        return x;
+    };
     // block index of this lane in group grp (n: none): list position j = grp * BPW + lane, found in
     // its sub-list by a wave-uniform search for the group's first position and a walk over the
     // (usually no) sub-list ends the group spans; one load, issued a group before the descriptor
@@ -450,11 +469,11 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
         const bool ok = lane < BPW && j < cnt;
         if (natural) return ok ? j : n;
         uint32_t sidx = 0;
-        for (uint32_t step = 32; step; step >>= 1)
+        for (uint32_t step = NSUB / 2; step; step >>= 1)
             if (rl(incl, sidx + step - 1) <= j0) sidx += step;
         uint32_t sl = sidx, b0 = rl(excl, sidx);
         const uint32_t jl = j0 + BPW - 1 < cnt - 1 ? j0 + BPW - 1 : cnt - 1;
-        for (uint32_t t = sidx; t < 63; t++) {
+        for (uint32_t t = sidx; t < NSUB - 1; t++) {
             const uint32_t it = rl(incl, t);
             if (it > jl) break;
             if (j >= it) {
@@ -580,7 +599,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     }
 }
 
-template <int BPW, int SLOT, int CH, int ORDER>
+template <int BPW, int SLOT, int CH, int ORDER, int NSUB>
 static hipError_t launch_snappy_tier(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h,
                                      uint32_t n, bhg_desc *out, uint8_t *out_vals, uint64_t out_cap,
                                      const uint64_t *val_off, const uint32_t *in_cnt, const uint32_t *in_ent,
@@ -588,12 +607,12 @@ static hipError_t launch_snappy_tier(const Launch &L, const uint8_t *src, uint64
     // resident workgroups per CU (LDS-bound); a grid past that would start its extra
     // workgroups only when the first ones finish
     static const uint32_t per_cu =
-        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, ORDER>, 64, (160u * 1024u) / (BPW * SLOT + 64));
+        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, ORDER, NSUB>, 64, (160u * 1024u) / (BPW * SLOT + 64));
     const uint32_t groups = (n + BPW - 1) / BPW;
     const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
     uint32_t grid = groups < cap ? groups : cap;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, ORDER>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, ORDER, NSUB>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
                        out_vals, out_cap, val_off, in_cnt, in_ent, sub_cap, out_cnt, out_ent);
     return hipGetLastError();
 }
@@ -605,16 +624,16 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         // the lists the header pass filled (launch_decode with the same pointer; layout in
         // bhg_internal.h): the <= 1-KiB class, the 1-4 KiB class, and the global-memory list
         const uint32_t cap = (uint32_t)snappy_sub_cap(n);
-        uint32_t *c_small = list, *c_large = list + 64, *c_rt = list + 128;
+        uint32_t *c_small = list, *c_large = list + 64, *c_rt = list + kSnapRtCount;
         uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * cap,
-                 *e_rt = e_large + (size_t)64 * cap;
-        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 2>(L, src, src_len, h, n, out, out_vals, out_cap,
+                 *e_rt = e_large + (size_t)64 * kSnapBuckets * cap;
+        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 2, 64>(L, src, src_len, h, n, out, out_vals, out_cap,
                                                                      val_off, c_small, e_small, cap, c_rt, e_rt))
             return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 1>(L, src, src_len, h, n, out, out_vals, out_cap,
+        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 1, 64>(L, src, src_len, h, n, out, out_vals, out_cap,
                                                                      val_off, c_small, e_small, cap, c_rt, e_rt))
             return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, 0>(L, src, src_len, h, n, out, out_vals,
+        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, 0, 64 * kSnapBuckets>(L, src, src_len, h, n, out, out_vals,
                                                                          out_cap, val_off, c_large, e_large, cap,
                                                                          c_rt, e_rt))
             return e;

@@ -93,9 +93,9 @@ def test_shipped_library_has_default_knobs():
     want = {
         rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf)},
         # the LDS tiers: 1-KiB slots in the batch's order or from the header pass's list, 4-KiB slots
-        rb"_ZN3bhg12k_snappy_ldsI": {b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi2EE" % (bpw, slot),
-                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi1EE" % (bpw, slot),
-                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi%dELi0EE" % (bpw2, slot2, ch2)},
+        rb"_ZN3bhg12k_snappy_ldsI": {b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi2ELi64EE" % (bpw, slot),
+                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi1ELi64EE" % (bpw, slot),
+                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi%dELi0ELi256EE" % (bpw2, slot2, ch2)},
     }
     for prefix, names in want.items():
         found = set(re.findall(re.escape(prefix) + rb"[A-Za-z0-9]+?EE", blob))
