@@ -241,9 +241,6 @@ __global__ __launch_bounds__(256) void k_snappy_rt(const uint8_t *__restrict__ s
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSlBpw = 18;     // blocks (lanes) per wave
 constexpr uint32_t kSlSlot = 1088;  // in-place slot bytes per block
-constexpr uint32_t kSlBpw2 = 6;      // tier 2 (values up to 4 KiB)
-constexpr uint32_t kSlSlot2 = 4160;
-constexpr uint32_t kSlCh2 = 2;
 
 // Every LDS access of k_snappy_lds goes through these may_alias types: the slot
 // is written as 16-B chunks and read as bytes, 8-B tags and 16-B chunks, and
@@ -391,39 +388,40 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 
 }  // namespace
 
-// Two tiers of the same kernel: <18, 1,088, 1> takes the blocks that decode to <= 1 KiB,
-// <6, 4,160, 2> the others, each from the header pass's 64 sub-lists of its size class
-// (launch_decode; in_cnt: the 64 sub-list sizes, in_ent: sub-list 0, sub_cap entries apart), and
-// k_snappy_rt what neither holds (out_cnt / out_ent: the blocks a tier hands on).  CH: 16-B
-// stream chunks per lane per block prefetched into VGPRs (the rest of a longer stream is loaded
-// at the dump).
+// The LDS walk runs in "roles": a slot shape (BPW blocks per wave in SLOT-byte in-place slots, CH
+// 16-B stream chunks per lane per block prefetched into VGPRs, the rest of a longer stream loaded
+// at the dump) over one list of blocks.  The header pass (k_decode_stream<1>) sorted the blocks to
+// decode into 64 sub-lists per class (in_cnt: the sub-lists' sizes, in_ent: sub-list 0, sub_cap
+// entries apart): <= 1 KiB decoded with the stream fitting 1,088 B (tier 1), and 4 buckets of
+// decoded size above it (tier 2).  k_snappy_lds_nat walks the batch in its own order when >= 7/8
+// of it is small (C3); k_snappy_lds_multi runs every list in one launch, largest slots first: the
+// buckets in 4,160 / 3,392 / 2,624 / 1,856-B slots (6 / 7 / 9 / 13 blocks per wave), then tier 1's
+// list (23 per wave) unless the batch went in its own order.  What neither holds (over 4 KiB, an
+// in-place spill) goes to k_snappy_rt (out_cnt / out_ent).
 // Measured on the C4-shaped decode (bench.py --config mixdec: 1M values U[64, 4096], 76 % of
-// them > 1 KiB): the > 1 KiB blocks took 5.83 ms per step in k_snappy_rt; tier 2 takes 4.2 ms
-// (step 6.90 -> 5.27 ms, 137 -> 180 GiB/s).  Tier-2 shapes A/B'd (2 runs each, one box;
-// profiles/r5/snappy_t2): 6 blocks x 2 chunks 5.27 ms, 4 x 4 5.44, 3 x 4 5.52, 2 x 4 5.77; 64-B ops
-// (4 reads in flight per element) 6.3 ms and C3 +12 %; a 2-KiB class of 12 (or 9, 16) blocks per
-// wave for values <= 2 KiB 5.30-5.47 ms; one WAVE per block (wave-uniform SALU decode,
-// byte-per-lane copies) 7.3 ms for tier 2 alone -- ~75 SALU instructions per element for one
-// block, where a lane walk spends ~80 VALU per element step for 6.  Until round 5 tier 1 walked
-// every block (those it could not hold idled their lanes: 0.71 ms of the mixdec step for 24 % of
-// the blocks); the header pass now sorts them (mixdec 5.27 -> 4.89 ms), tier 2's by decoded size
-// into 4 buckets so that a wave's 6 lanes finish together (4.89 -> 4.28 ms; the tier was issue
-// bound, ~195 instructions per wave element step with the walk as long as its longest block).
-// ORDER: 0 the list (tier 2); 1 the list unless the batch is mostly this class, 2 the batch's
-// own order only when it is (tier 1: two launches, each returning at once when not its case, so
+// them > 1 KiB; profiles/r5/snappy_*): the > 1 KiB blocks took 5.83 ms per step in k_snappy_rt
+// (6.90-ms step, 137.6 GiB/s); one 4,160-B tier 5.27 ms per step; tier 1 from the header pass's
+// list instead of walking all blocks 4.89; tier 2 in size buckets 4.28; slots sized per bucket
+// 3.98; all lists in one launch 3.75-3.77 (252 GiB/s).  Dropped: 4 x 4 / 3 x 4 / 2 x 4 blocks x
+// chunks in the 4-KiB tier (5.44-5.77 vs 5.27), 64-B ops (4 reads in flight per element: 6.3 ms,
+// C3 +12 %), a 2-KiB class before the buckets (5.30-5.47), one WAVE per block (wave-uniform SALU
+// decode, byte-per-lane copies: 7.3 ms for the tier alone, ~75 SALU instructions per element for
+// one block where a lane walk spends ~80 VALU per element step for 6), 8 / 12 buckets.
+// ORDER: 0 the list; 1 the list unless the batch is mostly this class, 2 the batch's own order
+// only when it is (tier 1 in two kernels, each role returning at once when not its case, so
 // neither carries the other's code)
+// the work of one slot shape over its list (a "role"): lds holds BPW * SLOT + 64 bytes (+ 64:
+// literal reads past the last slot); the workgroup takes groups blockIdx.x, + gridDim.x, ...
 template <int BPW, int SLOT, int CH, int ORDER, int NSUB>
-__global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ src, uint64_t src_len,
-                                                   const bhg_handle *__restrict__ handles, uint32_t n,
-                                                   bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
-                                                   uint64_t out_cap, const uint64_t *__restrict__ val_off,
-                                                   const uint32_t *__restrict__ in_cnt,
-                                                   const uint32_t *__restrict__ in_ent, uint32_t sub_cap,
-                                                   uint32_t *__restrict__ out_cnt, uint32_t *__restrict__ out_ent) {
+__device__ __forceinline__ void sl_role(uint8_t *__restrict__ lds, const uint8_t *__restrict__ src, uint64_t src_len,
+                                        const bhg_handle *__restrict__ handles, uint32_t n,
+                                        bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals, uint64_t out_cap,
+                                        const uint64_t *__restrict__ val_off, const uint32_t *__restrict__ in_cnt,
+                                        const uint32_t *__restrict__ in_ent, uint32_t sub_cap,
+                                        uint32_t *__restrict__ out_cnt, uint32_t *__restrict__ out_ent) {
     static_assert(SLOT % 16 == 0, "16-B aligned slots");
     constexpr uint32_t DMAX = SLOT - 64;            // longest decoded block a slot takes
     constexpr uint32_t DCH = (DMAX + 1023) / 1024;  // 1-KiB rows of the store-out
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BPW * SLOT + 64];  // + 64: literal reads past the last slot
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)src, end = base + src_len;
     // the sub-lists as one list: lane k holds the inclusive / exclusive prefix of their sizes at k
@@ -599,22 +597,48 @@ __global__ __launch_bounds__(64) void k_snappy_lds(const uint8_t *__restrict__ s
     }
 }
 
-template <int BPW, int SLOT, int CH, int ORDER, int NSUB>
-static hipError_t launch_snappy_tier(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h,
-                                     uint32_t n, bhg_desc *out, uint8_t *out_vals, uint64_t out_cap,
-                                     const uint64_t *val_off, const uint32_t *in_cnt, const uint32_t *in_ent,
-                                     uint32_t sub_cap, uint32_t *out_cnt, uint32_t *out_ent) {
-    // resident workgroups per CU (LDS-bound); a grid past that would start its extra
-    // workgroups only when the first ones finish
-    static const uint32_t per_cu =
-        resident_per_cu((const void *)k_snappy_lds<BPW, SLOT, CH, ORDER, NSUB>, 64, (160u * 1024u) / (BPW * SLOT + 64));
-    const uint32_t groups = (n + BPW - 1) / BPW;
-    const uint32_t cap = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
-    uint32_t grid = groups < cap ? groups : cap;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_snappy_lds<BPW, SLOT, CH, ORDER, NSUB>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
-                       out_vals, out_cap, val_off, in_cnt, in_ent, sub_cap, out_cnt, out_ent);
-    return hipGetLastError();
+// tier 1 in the batch's own order (when >= 7/8 of the blocks are small; else it returns at once)
+__global__ __launch_bounds__(64) void k_snappy_lds_nat(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                       const bhg_handle *__restrict__ handles, uint32_t n,
+                                                       bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
+                                                       uint64_t out_cap, const uint64_t *__restrict__ val_off,
+                                                       const uint32_t *__restrict__ c_small,
+                                                       const uint32_t *__restrict__ e_small, uint32_t sub_cap,
+                                                       uint32_t *__restrict__ c_rt, uint32_t *__restrict__ e_rt) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kSlBpw * kSlSlot + 64];
+    sl_role<kSlBpw, kSlSlot, 1, 2, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
+                                       sub_cap, c_rt, e_rt);
+}
+
+// every list in one launch, largest slots first: the 4 size buckets of the 4-KiB tier, each in
+// slots sized to it, then tier 1's list (unless tier 1 ran in batch order).  One launch, so the
+// empty roles of an all-1-KiB batch cost one start-up, and a role's tail overlaps the next one's
+// groups.
+constexpr uint32_t kMultiLds = 23 * 1088 + 64;  // the largest role (6 x 4,160 + 64 = 25,024 B is next)
+__global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                         const bhg_handle *__restrict__ handles, uint32_t n,
+                                                         bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
+                                                         uint64_t out_cap, const uint64_t *__restrict__ val_off,
+                                                         uint32_t *__restrict__ list, uint32_t sub_cap) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
+    static_assert(kSnapBuckets == 4 && kSnapBucketBytes == 768, "the bucket slot sizes below");
+    static_assert(6 * 4160 + 64 <= kMultiLds && 7 * 3392 + 64 <= kMultiLds && 9 * 2624 + 64 <= kMultiLds && 13 * 1856 + 64 <= kMultiLds &&
+                      23 * 1088 + 64 <= kMultiLds, "roles fit the LDS");
+    const uint32_t *c_small = list, *c_large = list + 64;
+    uint32_t *c_rt = list + kSnapRtCount;
+    const uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * sub_cap;
+    uint32_t *e_rt = list + kSnapListHdr + (size_t)kSnapSubs * sub_cap;
+    const size_t bs = (size_t)64 * sub_cap;
+    sl_role<6, 4160, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large, e_large, sub_cap,
+                               c_rt, e_rt);
+    sl_role<7, 3392, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 64,
+                               e_large + bs, sub_cap, c_rt, e_rt);
+    sl_role<9, 2624, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 128,
+                               e_large + 2 * bs, sub_cap, c_rt, e_rt);
+    sl_role<13, 1856, 1, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 192,
+                                e_large + 3 * bs, sub_cap, c_rt, e_rt);
+    sl_role<23, 1088, 1, 1, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
+                                sub_cap, c_rt, e_rt);
 }
 
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
@@ -624,19 +648,25 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         // the lists the header pass filled (launch_decode with the same pointer; layout in
         // bhg_internal.h): the <= 1-KiB class, the 1-4 KiB class, and the global-memory list
         const uint32_t cap = (uint32_t)snappy_sub_cap(n);
-        uint32_t *c_small = list, *c_large = list + 64, *c_rt = list + kSnapRtCount;
-        uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * cap,
-                 *e_rt = e_large + (size_t)64 * kSnapBuckets * cap;
-        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 2, 64>(L, src, src_len, h, n, out, out_vals, out_cap,
-                                                                     val_off, c_small, e_small, cap, c_rt, e_rt))
-            return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw, kSlSlot, 1, 1, 64>(L, src, src_len, h, n, out, out_vals, out_cap,
-                                                                     val_off, c_small, e_small, cap, c_rt, e_rt))
-            return e;
-        if (hipError_t e = launch_snappy_tier<kSlBpw2, kSlSlot2, kSlCh2, 0, 64 * kSnapBuckets>(L, src, src_len, h, n, out, out_vals,
-                                                                         out_cap, val_off, c_large, e_large, cap,
-                                                                         c_rt, e_rt))
-            return e;
+        uint32_t *c_small = list, *c_rt = list + kSnapRtCount;
+        uint32_t *e_small = list + kSnapListHdr, *e_rt = list + kSnapListHdr + (size_t)kSnapSubs * cap;
+        {
+            static const uint32_t per_cu =
+                resident_per_cu((const void *)k_snappy_lds_nat, 64, (160u * 1024u) / (kSlBpw * kSlSlot + 64));
+            const uint32_t groups = (n + kSlBpw - 1) / kSlBpw, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
+            const uint32_t grid = groups < lim ? (groups ? groups : 1u) : lim;
+            hipLaunchKernelGGL(k_snappy_lds_nat, dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out, out_vals,
+                               out_cap, val_off, c_small, e_small, cap, c_rt, e_rt);
+            if (hipError_t e = hipGetLastError()) return e;
+        }
+        {
+            static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_lds_multi, 64, (160u * 1024u) / kMultiLds);
+            const uint32_t groups = (n + 5) / 6, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
+            const uint32_t grid = groups < lim ? (groups ? groups : 1u) : lim;
+            hipLaunchKernelGGL(k_snappy_lds_multi, dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out, out_vals,
+                               out_cap, val_off, list, cap);
+            if (hipError_t e = hipGetLastError()) return e;
+        }
         // then the blocks the tiers handed on (too big for a slot, or an in-place spill), lane per
         // block from global memory
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,

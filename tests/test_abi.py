@@ -87,16 +87,13 @@ def test_shipped_library_has_default_knobs():
     nch = _src_default("bhg_decode_tile.hip", "kTileNch")
     bpw = _src_default("bhg_snappy_dec.hip", "kSlBpw")
     slot = _src_default("bhg_snappy_dec.hip", "kSlSlot")
-    bpw2 = _src_default("bhg_snappy_dec.hip", "kSlBpw2")
-    slot2 = _src_default("bhg_snappy_dec.hip", "kSlSlot2")
-    ch2 = _src_default("bhg_snappy_dec.hip", "kSlCh2")
     want = {
         rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf)},
-        # the LDS tiers: 1-KiB slots in the batch's order or from the header pass's list, 4-KiB slots
-        rb"_ZN3bhg12k_snappy_ldsI": {b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi2ELi64EE" % (bpw, slot),
-                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi1ELi1ELi64EE" % (bpw, slot),
-                                     b"_ZN3bhg12k_snappy_ldsILi%dELi%dELi%dELi0ELi256EE" % (bpw2, slot2, ch2)},
     }
+    # the snappy LDS tiers: tier 1 in batch order, and one multi-role launch for the lists
+    assert b"_ZN3bhg16k_snappy_lds_natE" in blob and b"_ZN3bhg18k_snappy_lds_multiE" in blob
+    assert not re.search(rb"_ZN3bhg12k_snappy_ldsI", blob)
+    assert _src_default("bhg_snappy_dec.hip", "kSlBpw") == 18 and slot == 1088
     for prefix, names in want.items():
         found = set(re.findall(re.escape(prefix) + rb"[A-Za-z0-9]+?EE", blob))
         assert found == names, (prefix, found, names)
