@@ -12,8 +12,8 @@ values with out_val_off past 4 GiB.  Checks:
   * every status OK (the expected CRCs are the writer's);
   * the one-launch digest equals the sum of the per-table digests, each table
     decoded by its own launch;
-  * tables 0 and 183 bit-exact against the restatement (descriptors, and the
-    decoded bytes for snappy);
+  * every table bit-exact against the restatement (descriptors, and the
+    decoded bytes for snappy), one table at a time on the host;
   * snappy: every decoded value equals the generator's input value.
 """
 import numpy as np
@@ -93,7 +93,7 @@ def test_c5_none_one_launch(codec):
                                    expected_crc=exp_crc[t * R:(t + 1) * R])
             summed = _add(summed, _digest(r.desc_np()))
         assert summed == whole
-        for t in (0, T - 1):
+        for t in range(T):
             _check_table_vs_restatement(src_t, h, exp_crc, d, t, snappy=False)
         del src_t, h_t, exp_crc, res
     torch.cuda.empty_cache()
@@ -133,7 +133,7 @@ def test_c5_snappy_one_launch(codec):
                                    expected_crc=exp_crc[rows], out_vals=tv)
             summed = _add(summed, _digest(r.desc_np()))
         assert summed == whole
-        for t in (0, T - 1):
+        for t in range(T):
             _check_table_vs_restatement(src_t, h, exp_crc, d, t, snappy=True, vals_t=vals_t, voff=voff)
         del src_t, h_t, exp_crc, vals_t, res
     torch.cuda.empty_cache()
