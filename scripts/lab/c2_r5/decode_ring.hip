@@ -1,4 +1,4 @@
-// bhg_decode_ring.hip -- NoCompressor batch decode as an LDS-DMA loader / consumer ring (gfx950).
+// decode_ring.hip (lab, round 5; not built into the product) -- NoCompressor batch decode as an LDS-DMA loader / consumer ring (gfx950).
 //
 // Same outputs as k_decode_tile (readRecord + readKV + FNV-1 + masked CRC-32C per handle;
 // bithash/block2.go:31-66, reader.go:233-272, compress.go:57-59, internal/hash/fnv.go:19-23,
@@ -34,9 +34,9 @@
 //     CRC check; descriptor.  CRC linearity over GF(2): crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B).
 // CRC tables: CrcR8 (slice-by-4, 8 replicas, 32 KiB, conflict free) + 6 shift tables (24 KiB);
 // the ring (11 x 9 KiB) beside them: 156 KiB of LDS, one workgroup per CU.
-#include "bhg_crc_tables.h"
-#include "bhg_device.h"
-#include "bhg_internal.h"
+#include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
+#include "../../../bitalosdb_amd/csrc/bhg_device.h"
+#include "../../../bitalosdb_amd/csrc/bhg_internal.h"
 
 namespace bhg {
 namespace ring {

@@ -1,5 +1,5 @@
 // ring_lab.hip -- development harness (not product code): the LDS-DMA ring decode
-// (bitalosdb_amd/csrc/bhg_decode_ring.hip) checked descriptor for descriptor against the product
+// (decode_ring.hip) checked descriptor for descriptor against the product
 // library's bhg_decode_batch and timed beside it, on
 //   c2      BASELINE configs[1]: 1M x 1,076-B records in 128 MiB tables, expected CRCs, a few bad
 //           handles / records / CRCs;
@@ -16,7 +16,7 @@
 #include <random>
 #include <vector>
 
-#include "../../../bitalosdb_amd/csrc/bhg_decode_ring.hip"
+#include "decode_ring.hip"
 
 #define CK(x)                                                                                  \
     do {                                                                                       \
