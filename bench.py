@@ -206,11 +206,15 @@ def traffic_fields(cfg_args, kernels, alg_bytes_per_launch, what):
 
 
 BACKEND = "nccl"
+# a process group is up: N > 1, or the one-rank rehearsal of the N > 1 path (BHG_BENCH_PG1=1 at
+# --gpus 1: RCCL init, barriers, all-reduces and all-gathers on one real GPU; the line is then the
+# N > 1 line's shape, with its collectives run by a world of one)
+PG = False
 
 
 def dist_barrier(world, local):
     """Barrier of the N>1 bench (nccl: on the rank's device stream; gloo: host)."""
-    if world > 1:
+    if PG:
         import torch.distributed as dist
         if BACKEND == "nccl":
             dist.barrier(device_ids=[local])
@@ -220,7 +224,7 @@ def dist_barrier(world, local):
 
 def dist_sum_(t, world):
     """In-place SUM all-reduce of a small tensor (gloo: through host memory)."""
-    if world > 1:
+    if PG:
         import torch.distributed as dist
         if BACKEND == "nccl":
             dist.all_reduce(t)
@@ -300,11 +304,17 @@ def main():
     import torch.distributed as dist
     if a.config == "spawncheck":
         return spawn_check(a, world, rank)
-    global BACKEND
+    global BACKEND, PG
     BACKEND = a.backend
     if a.backend == "gloo":   # rehearsal: ranks may share a GPU
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    PG = world > 1 or os.environ.get("BHG_BENCH_PG1") == "1"
+    if PG:
+        if world == 1:
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         torch.cuda.set_device(local)
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -320,7 +330,7 @@ def main():
     with torch.cuda.stream(codec.stream):      # every torch op and event on the codec's HIP stream
         run(a, world, rank, local, dev, codec)
     codec.close()
-    if world > 1:
+    if PG:
         dist.destroy_process_group()
 
 
@@ -362,7 +372,7 @@ def run(a, world, rank, local, dev, codec):
         return run_c5(a, world, rank, local, dev, codec)
     if a.config == "c1":
         return run_c1(a, world, rank, local, dev, codec)
-    if world > 1:
+    if PG:
         # N > 1: the fixed 25 GB corpus split by table over the N GPUs (strong scaling), with
         # the per-GPU C2 batch (weak scaling) nested
         res = c5_measure(a, world, rank, local, dev, codec, "none", with_cpu=False)
@@ -1092,12 +1102,12 @@ def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
                      "step_avg_ms": round(step_ms, 4)},
         "status_ok_blocks": int(ok_total), "valid": bool(ok_total == n_total == T * R),
         "digest_all_ranks": "%016x" % digest_all, "ranks_seen": int(ranks.item()),
-        "backend": BACKEND if world > 1 else None,
+        "backend": BACKEND if PG else None,
     }
     if snappy:
         out["decoded_GiBps"] = round(raw_total * a.steps / el_max / 2 ** 30, 3)
         out["config"]["values"] = a.values
-    if world > 1:
+    if PG:
         out.update(shard.scaling_fields(elapsed, achieved / HBM_PEAK_GBPS, dev))
     if rank == 0 and world == 1 and with_cpu and not a.no_cpu and n:
         from oracle import oracle as O

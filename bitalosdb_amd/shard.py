@@ -42,7 +42,7 @@ def block_digest(crc, fnv1, trailer, status):
 def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
     """MAX of elapsed, SUM of block counts, per-rank digests added as two 32-bit
     lanes mod 2^32 (block_digest); returns python values.  Runs outside the timed region."""
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    multi = dist.is_available() and dist.is_initialized()  # a world of one too (the RCCL rehearsal)
     if multi and dist.get_backend() == "gloo":
         device = "cpu"   # gloo reduces host tensors
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
@@ -56,7 +56,7 @@ def reduce_stats(elapsed_s, ok_blocks, n_blocks, digest, device):
 
 def gather_floats(values, device):
     """Every rank's list of floats (all_gather; gloo through host tensors), rank order."""
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    multi = dist.is_available() and dist.is_initialized()  # a world of one too (the RCCL rehearsal)
     if multi and dist.get_backend() == "gloo":
         device = "cpu"
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)

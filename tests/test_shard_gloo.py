@@ -109,6 +109,21 @@ def test_single_process_reduce():
     assert (el, ok, n, dg) == (1.25, 7, 8, (5 << 32) | 9)
 
 
+def test_world1_group_runs_the_collectives():
+    """bench.py's one-rank rehearsal (BHG_BENCH_PG1=1) keeps a process group of one up, and the
+    shard reductions must run through it (not be skipped as 'single process') and return the
+    rank's own values; here on gloo, on the GPU box on RCCL (profiles/r5/pg1/)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), q))
+    p.start()
+    r, mine, s, el, ok, n, dg = q.get(timeout=120)
+    p.join(60)
+    assert p.exitcode == 0
+    assert mine == list(range(9)) and s == 900
+    assert (el, ok, n, dg) == (0.5, 900, 900, 1000)
+
+
 def _bench(args, env_extra=None, timeout=180):
     import subprocess
     import sys
