@@ -371,6 +371,47 @@ def test_snappy_small_majority_with_large_minority(codec):
         assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 130, 4097])
+def test_snappy_lists_shuffled_duplicates_small_batches(codec, n):
+    """The header pass files each block into a decode list by its wave's tile (sub-list =
+    tile mod 64), and the roles read the lists back by a per-wave binary search over the
+    sub-list sizes: batch sizes around the wave and sub-list boundaries (1 .. 4,097 handles,
+    4,097 = one handle past 64 tiles), handles in shuffled order with duplicates (one record
+    decoded into two output slots), every size class present."""
+    rng = random.Random(1000 + n)
+    streams = []
+    for i in range(min(n, 400)):
+        k = i % 6
+        if k == 0:
+            streams.append(O.snappy_encode(compressible(rng, rng.randrange(1025, 4097))))
+        elif k == 1:
+            streams.append(O.snappy_encode(compressible(rng, rng.choice([4097, 7000]))))
+        elif k == 2:
+            streams.append(O.snappy_encode(rand_bytes(rng, rng.choice([900, 1024, 2000]))))
+        elif k == 3:
+            streams.append(O.snappy_encode(compressible(rng, rng.randrange(0, 1025)))[:-1] if i % 12 == 3
+                           else O.snappy_encode(compressible(rng, rng.randrange(0, 1025))))
+        else:
+            streams.append(O.snappy_encode(compressible(rng, rng.randrange(1, 1025))))
+    src = bytearray()
+    recs = []
+    for i, st in enumerate(streams):
+        rec = O.record_set(b"sl-%d" % i, 1 << 8 | 1, st, 5)
+        recs.append((len(src), len(rec), 0))
+        src += rec
+    pick = [rng.randrange(len(recs)) for _ in range(n)]
+    if n >= 2:
+        pick[-1] = pick[0]                     # a duplicate handle at the far end of the batch
+    h = np.array([recs[j] for j in pick], dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    for i in range(n):
+        if exp["status"][i] == 0:
+            assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
+
+
 def _view_with_bit31(nbytes, dev):
     """A uint8 device view of nbytes whose address has bit 31 of its low word set
     over its whole length (low word in [0x80000100, 0xFFFFFFFF])."""
