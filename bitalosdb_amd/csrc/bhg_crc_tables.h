@@ -192,17 +192,17 @@ inline void build_tile_ztab(uint32_t *out) {
 // in this order.
 enum XTab : uint32_t { XZ16, XZ32, XZ64, XZ128, XZ256, XZ512, XZ1024, XTAB_N };
 constexpr uint64_t kXTabLen[XTAB_N] = {16, 32, 64, 128, 256, 512, 1024};
-// then the long-range checksum's span combine (k_crc_long_part / _join, bhg_decode.hip):
-// Z_{2^(10 + j)}, j = 0 .. kXLongN - 1 (1 KiB .. 4 GiB), from word kXLong on
-constexpr uint32_t kXLongN = 23;
+// then the long-range checksum's chain folds and span combine (k_crc_long_part / _join,
+// bhg_decode.hip): Z_{2^(kXLongLo + j)}, j = 0 .. kXLongN - 1 (64 B .. 2 GiB), from word kXLong on
+constexpr uint32_t kXLongLo = 6, kXLongN = 26;
 constexpr uint32_t kXLong = XTAB_N * 1024;
 constexpr uint32_t kXTabWords = kXLong + kXLongN * 1024;
 inline void build_xtab(uint32_t *out) {
     for (uint32_t k = 0; k < XTAB_N; k++) crc32c_shift_table(kXTabLen[k], out + 1024 * k);
-    for (uint32_t j = 0; j < kXLongN; j++) crc32c_shift_table(1ull << (10 + j), out + kXLong + 1024 * j);
+    for (uint32_t j = 0; j < kXLongN; j++) crc32c_shift_table(1ull << (kXLongLo + j), out + kXLong + 1024 * j);
 }
 
-// Shift tables of the LDS-DMA ring decode (bhg_decode_ring.hip), in this order: Z_32 and Z_68 (the
+// Shift tables of the LDS-DMA ring decode (lab: scripts/lab/c2_r5/decode_ring.hip), in this order: Z_32 and Z_68 (the
 // folds of a 136-B window's four chains), then Z_{136 * 2^k}, k = 0..3 (136 .. 1,088 B): a lane's
 // distance to the record end (k = 0..2), the Horner step over 8 windows (Z_1088), and the head's
 // shift past m - 1 windows by the bits of m - 1 (bits above 3 as repeated Z_1088).

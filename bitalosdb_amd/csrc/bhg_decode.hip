@@ -53,28 +53,72 @@ __global__ __launch_bounds__(256) void k_fnv_ranges(const uint8_t *__restrict__ 
 // indexhash_checksum of SURVEY 8(a) A6(ii): writer.go:476-478 stores
 // crc.New(indexhash_data).Value() (internal/crc/crc.go:23-33); a table open re-computes it,
 // and the table tail (bhg_tail.hip) writes it.  A range is cut into 64 x 256 spans of
-// 2^(10+s) bytes aligned to its END (s the smallest with 64 x 256 x 2^(10+s) >= its length),
+// 2^(8+s) bytes aligned to its END (s the smallest with 64 x 256 x 2^(8+s) >= its length),
 // so every span is full except the first non-empty one, which starts at byte 0 and runs from
-// Go's initial state ^0; every other span runs from state 0.  A lane CRCs one span; then, by
-// CRC linearity over GF(2),
+// Go's initial state ^0; every other span runs from state 0.  A lane CRCs one span as four
+// interleaved chains over its quarters (chain 0 from the span's initial state, the others
+// from 0), folded with Z_{quarter}; a partial first span runs as one chain.  Then, by CRC
+// linearity over GF(2),
 //     crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B),
 // a workgroup (one of 64 parts) folds its 256 span states as a tree whose right subtrees are
 // always full (level l shifts by Z_{2^l spans}), and one wave per range folds the 64 part
 // states the same way (Z_{2^(8+l) spans}).  Empty spans left of the first hold 0, and Z(0) = 0.
-// The shift tables Z_{2^(10+j)} come from the context (bhg_crc_tables.h kXLong).  Round 3's
-// one-workgroup-per-range kernel took ~0.6 ms for a 10-MB index (one CU); this spreads a range
-// over up to 64 workgroups.
-constexpr uint32_t kLongParts = 64, kLongThreads = 256;
+// The shift tables Z_{2^(6+j)} come from the context (bhg_crc_tables.h kXLong).
+// History: round 3's one-workgroup-per-range kernel took ~0.6 ms for a 10-MB index (one CU);
+// round 4 spread a range over up to 64 workgroups with one serial 1-KiB chain per lane (23 x
+// 1.51 MB: 0.057 ms, the chain's dependent LDS lookups); round 5: 256-B spans, four chains
+// (0.0295 ms; k_crc_long_part 21.8-23.5 us + k_crc_long_join 4.1-4.5 us).
+// 256 lanes per part: 512 (8 waves, two workgroups per CU) measured 28.5 against 23.5 us, and
+// the conflict-free CrcR8 (two VALU per lookup address) 27.8 against Crc4Lds<8>'s 23.5 us
+// (23 x 1.51 MB, profiles/r5/crc_long/)
+constexpr uint32_t kLongTLog = 8;  // log2 of the spans (lanes) per part
+constexpr uint32_t kLongParts = 64, kLongThreads = 1u << kLongTLog, kLongSpan0 = 8;
+// every shift the kernels take exists: the quarter fold Z_{2^(6+s)} up to the join's last level
+// Z_{2^31} (64 x 256 spans of 2^18 B at s = 10 cover any u32 length)
+static_assert(kLongSpan0 - 2 >= kXLongLo && 31 - kXLongLo < kXLongN, "long shift set");
 
 __device__ __forceinline__ uint32_t zapply_tab(const uint32_t *Zt, uint32_t c) {
     return Zt[c & 255u] ^ Zt[256 + ((c >> 8) & 255u)] ^ Zt[512 + ((c >> 16) & 255u)] ^ Zt[768 + (c >> 24)];
 }
 
-// the range's span exponent s and span count (spans of 2^(10+s) bytes covering len)
+// the range's span exponent s and span count (spans of 2^(8+s) bytes covering len)
 __device__ __forceinline__ void long_geo(uint64_t len, uint32_t &s, uint64_t &nspan) {
     s = 0;
-    while (((uint64_t)kLongParts * kLongThreads << (10 + s)) < len) s++;
-    nspan = (len + (1ull << (10 + s)) - 1) >> (10 + s);
+    while (((uint64_t)kLongParts * kLongThreads << (kLongSpan0 + s)) < len) s++;
+    nspan = (len + (1ull << (kLongSpan0 + s)) - 1) >> (kLongSpan0 + s);
+}
+
+// Z_{2^x} in the context's long set
+__device__ __forceinline__ const uint32_t *zlong(const uint32_t *zl, uint32_t x) {
+    return zl + (uint64_t)(x - kXLongLo) * 1024;
+}
+
+// raw CRC of the full span [A, A + 2^(8+s)) (any alignment, inside the source): four chains over
+// its quarters of 2^(6+s) bytes, 64 B of each per step, chain 0 from c0; folded with Zq = Z_quarter
+template <class Tab>
+__device__ __forceinline__ uint32_t span_crc4(const Tab &crc, const uint32_t *Zq, uint32_t c0, uint64_t A, uint32_t s,
+                                              uint64_t end) {
+    const uint64_t aa = A & ~3ull, Q = 64ull << s;
+    const uint32_t z = (uint32_t)(A & 3);
+    uint32_t cc[4] = {c0, 0u, 0u, 0u};
+    for (uint32_t it = 0; it < (1u << s); it++) {
+        uint32_t w[4][17];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t a = aa + (uint64_t)j * Q + 64ull * it;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4 x = gld<u32x4_a4>(a + 16 * q);  // inside the span: below end
+                w[j][4 * q] = x.x; w[j][4 * q + 1] = x.y; w[j][4 * q + 2] = x.z; w[j][4 * q + 3] = x.w;
+            }
+            w[j][16] = z ? ld32_safe(a + 64, end) : 0u;  // the last quarter's may pass the source end
+        }
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) cc[j] = crc.word(cc[j], __builtin_amdgcn_alignbyte(w[j][t + 1], w[j][t], z));
+    }
+    return zapply_tab(Zq, zapply_tab(Zq, zapply_tab(Zq, cc[0]) ^ cc[1]) ^ cc[2]) ^ cc[3];
 }
 
 __global__ __launch_bounds__(kLongThreads) void k_crc_long_part(const uint8_t *__restrict__ src, uint64_t src_len,
@@ -94,23 +138,28 @@ __global__ __launch_bounds__(kLongThreads) void k_crc_long_part(const uint8_t *_
         return;
     }
     __shared__ __attribute__((aligned(16))) uint32_t T[Crc4Lds<8>::kWords];
-    __shared__ uint32_t Z[8 * 1024], st[kLongThreads];
     Crc4Lds<8>::fill(T);
-    for (uint32_t w = t; w < 8 * 1024; w += kLongThreads) Z[w] = zl[(uint64_t)s * 1024 + w];  // Z_{span 2^l}, l = 0..7
-    __syncthreads();
     const Crc4Lds<8> crc(T);
+    __shared__ uint32_t Z[kLongTLog * 1024], Zq[1024], st[kLongThreads];
+    const uint32_t *zs = zlong(zl, kLongSpan0 + s);  // Z_{span 2^l}, l < kLongTLog: contiguous in the set
+    for (uint32_t w = t; w < kLongTLog * 1024; w += kLongThreads) Z[w] = zs[w];
+    const uint32_t *zq = zlong(zl, kLongSpan0 - 2 + s);  // Z_{span / 4}
+    for (uint32_t w = t; w < 1024; w += kLongThreads) Zq[w] = zq[w];
+    __syncthreads();
     const uint64_t g = (uint64_t)p * kLongThreads + t;
     uint32_t c = 0;
     if (g >= first) {
-        const uint64_t span = 1ull << (10 + s), k = g - first;  // k: span index from the range start
-        const uint64_t e = len - (nspan - 1 - k) * span;       // end of the span (exclusive)
+        const uint64_t span = 1ull << (kLongSpan0 + s), k = g - first;  // k: span index from the range start
+        const uint64_t e = len - (nspan - 1 - k) * span;               // end of the span (exclusive)
         const uint64_t b = k == 0 ? 0 : e - span;
-        c = crc_range(crc, k == 0 ? 0xffffffffu : 0u, (uint64_t)src + h.offset + b, e - b, (uint64_t)src + src_len);
+        const uint64_t A = (uint64_t)src + h.offset + b, end = (uint64_t)src + src_len;
+        if (e - b == span) c = span_crc4(crc, Zq, k == 0 ? 0xffffffffu : 0u, A, s, end);
+        else c = crc_range(crc, 0xffffffffu, A, e - b, end);  // a partial first span
     }
     st[t] = c;
     __syncthreads();
 #pragma unroll
-    for (uint32_t l = 0; l < 8; l++) {
+    for (uint32_t l = 0; l < kLongTLog; l++) {
         const uint32_t w = 1u << l;
         if ((t & (2 * w - 1)) == 2 * w - 1) st[t] = zapply_tab(Z + l * 1024, st[t - w]) ^ st[t];
         __syncthreads();
@@ -134,7 +183,7 @@ __global__ __launch_bounds__(64) void k_crc_long_join(uint64_t src_len, const bh
     for (uint32_t l = 0; l < 6; l++) {
         const uint32_t w = 1u << l;
         const uint32_t left = __shfl(v, (int)(lane >= w ? lane - w : 0), 64);
-        if ((lane & (2 * w - 1)) == 2 * w - 1) v = zapply_tab(zl + (uint64_t)(s + 8 + l) * 1024, left) ^ v;
+        if ((lane & (2 * w - 1)) == 2 * w - 1) v = zapply_tab(zlong(zl, kLongSpan0 + s + kLongTLog + l), left) ^ v;  // 2^l parts
     }
     if (lane == 63) {
         const uint32_t state = len ? v : 0xffffffffu;  // crc.New of nothing: ^0

@@ -27,8 +27,10 @@ def codec():
 
 
 def test_long_ranges_match_restatement(codec):
-    """Span-boundary lengths (1 KiB spans aligned to the range end, 64 x 256 of them before the
-    span doubles at 16 MiB), odd alignments, empty and out-of-range handles."""
+    """Span-boundary lengths (256-B spans aligned to the range end, 64 x 256 of them before the
+    span doubles at 4 MiB, 8 MiB, 16 MiB ...; four chains per full span, one for a partial
+    first span; round 4's 1-KiB spans kept in the list), odd alignments, empty and out-of-range
+    handles, a range ending at the last byte of the source."""
     from bitalosdb_amd.codec import as_device_bytes, handles_tensor
     rng = np.random.default_rng(21)
     size = 20 << 20
@@ -36,14 +38,18 @@ def test_long_ranges_match_restatement(codec):
     dsrc = as_device_bytes(data, codec.device)
     K = 4096
     M16 = 16 << 20
-    lens = [0, 1, 3, 4, 5, 63, 1023, 1024, 1025, 4095, K, K + 1, 2 * K - 1, 2 * K, 2 * K + 1, 1_510_000,
-            2048 * K - 1, 2048 * K, 2048 * K + 1, M16 - 1, M16, M16 + 1, M16 + 1023, M16 + 1025, 17 << 20]
+    M4 = 4 << 20
+    lens = [0, 1, 3, 4, 5, 63, 64, 255, 256, 257, 511, 512, 513, 767, 1023, 1024, 1025, 4095, K, K + 1,
+            2 * K - 1, 2 * K, 2 * K + 1, 1_510_000, M4 - 1, M4, M4 + 1, M4 + 255, M4 + 257, 2 * M4 - 1,
+            2 * M4 + 1, 2048 * K - 1, 2048 * K, 2048 * K + 1, M16 - 1, M16, M16 + 1, M16 + 1023, M16 + 1025,
+            17 << 20]
     hs = []
     for ln in lens:
         for off in (0, 1, 2, 3, 1001):
             if off + ln <= size:
                 hs.append((off, ln, 0))
-    hs += [(size, 0, 0), (size - 10, 11, 0), (size + 1, 0, 0), (0, size, 0)]
+    hs += [(size, 0, 0), (size - 10, 11, 0), (size + 1, 0, 0), (0, size, 0), (1, size - 1, 0),
+           (size - 4099, 4099, 0), (size - M4 - 3, M4 + 3, 0)]
     h = np.array(hs, dtype=O.HANDLE_DT)
     got = codec.crc_long(dsrc, handles_tensor(h, codec.device), len(h)).cpu().numpy().view(np.uint32)
     short = codec.crc_batch(dsrc, handles_tensor(h, codec.device), len(h)).cpu().numpy().view(np.uint32)
