@@ -1142,8 +1142,10 @@ int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, u
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
     Scratch sc;
-    if (int r = scratch_alloc(c, L.stream, bhg::scan_scratch_bytes(ntables), sc)) return r;
-    HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, sc.base));
+    const size_t sb = (bhg::scan_scratch_bytes(ntables) + 255) & ~(size_t)255;
+    if (int r = scratch_alloc(c, L.stream, sb + bhg::tscan_uni_bytes(ntables), sc)) return r;
+    HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, sc.base,
+                                 static_cast<uint8_t *>(sc.base) + sb));
     return BHG_OK;
 }
 

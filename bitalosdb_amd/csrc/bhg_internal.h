@@ -185,9 +185,11 @@ hipError_t launch_add_u64(const Launch &L, uint64_t *p, uint64_t n, uint64_t add
 // dst (mapped host memory) <- src, n bytes; src == dst mod 16
 hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, uint64_t n);
 
-// bhg_tscan.hip: table data-region scan (count -> scan -> write); first[ntables+1],
-// scan_scratch holds scan_scratch_bytes(ntables).
+// bhg_tscan.hip: table data-region scan (uniform prefixes -> count -> scan -> write); first[ntables+1],
+// scan_scratch holds scan_scratch_bytes(ntables), uni_scratch tscan_uni_bytes(ntables).
+size_t tscan_uni_bytes(uint32_t ntables);
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
-                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch);
+                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
+                        void *uni_scratch);
 
 }  // namespace bhg

@@ -16,6 +16,14 @@
 //    at LDS latency.
 // The scan runs twice: count per table -> exclusive scan (out_first) ->
 // the same walk again writing the handles.
+//
+// Before the walk, k_tscan_uni finds each table's UNIFORM PREFIX with every CU
+// at once: the first F records from offset 0 whose length is the first record's
+// G0 (record i at i * G0; the first record that is not -- a different length or
+// a stop rule -- is F, a true record start, since records 0..F-1 are).  A
+// bulk-loaded table is one uniform prefix ended by its terminating stop, so the
+// one-workgroup walk only starts at record F; the F handles are written by a
+// grid-wide pass (k_tscan_uni<true>).
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -62,11 +70,53 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *s) {
     return (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
 }
 
+// uniform prefix per table: uni[t] = F (atomic min over the failing record indices; the
+// caller sets uni to ~0 first).  WRITE: the F handles of every table at out[first[t] + i].
+constexpr int TU_THREADS = 256, TU_PARTS = 64;  // workgroups per table
+template <bool WRITE>
+__global__ __launch_bounds__(TU_THREADS) void k_tscan_uni(const uint8_t *__restrict__ src,
+                                                          const uint64_t *__restrict__ table_off, int mode,
+                                                          unsigned long long *__restrict__ uni,
+                                                          bhg_handle *__restrict__ out, uint64_t max_out,
+                                                          const uint64_t *__restrict__ first) {
+    const uint32_t t = blockIdx.y, lane = threadIdx.x & 63;
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase;
+    const Hdr h0 = read_hdr_global(t0, tlen, 0, mode);
+    const uint64_t G = h0.stop ? 0 : h0.adv;
+    const uint64_t step = (uint64_t)TU_PARTS * TU_THREADS;
+    const uint64_t i0 = (uint64_t)blockIdx.x * TU_THREADS + threadIdx.x;
+    if (WRITE) {
+        const uint64_t F = uni[t], w0 = first[t];
+        for (uint64_t i = i0; i < F && w0 + i < max_out; i += step) out[w0 + i] = bhg_handle{tbase + i * G, (uint32_t)G, 0};
+        return;
+    }
+    if (G == 0) {  // record 0 ends the scan: no prefix
+        if (i0 == 0) atomicMin(uni + t, 0ull);
+        return;
+    }
+    // record tlen / G cannot have length G (it would end past the table), so F <= tlen / G
+    const uint64_t last = tlen / G;
+    for (uint64_t i = i0; i - lane <= last; i += step) {  // whole waves iterate together
+        bool bad = false;
+        if (i <= last) {
+            const Hdr h = read_hdr_global(t0, tlen, i * G, mode);
+            bad = h.stop || h.adv != G;
+        }
+        const uint64_t m = __ballot(bad);
+        if (m) {
+            if (lane == (uint32_t)__builtin_ctzll(m)) atomicMin(uni + t, (unsigned long long)i);
+            break;  // the wave's later records lie past a failure
+        }
+    }
+}
+
 template <bool WRITE>
 __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict__ src,
                                                       const uint64_t *__restrict__ table_off, int mode,
                                                       bhg_handle *__restrict__ out, uint64_t max_out,
-                                                      uint64_t *__restrict__ first, uint64_t *__restrict__ out_end) {
+                                                      uint64_t *__restrict__ first, uint64_t *__restrict__ out_end,
+                                                      const unsigned long long *__restrict__ uni) {
     __shared__ alignas(16) uint8_t win[TS_WIN];
     __shared__ uint32_t s_brk[2][TS_WAVES];
     __shared__ uint64_t s_adv[2][TS_WAVES];
@@ -80,6 +130,14 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
     const uint64_t w0 = WRITE ? first[t] : 0;
 
     uint64_t off = 0, cnt = 0, G = 0;
+    {  // start after the table's uniform prefix (k_tscan_uni): records 0..F-1 of length G0
+        const uint64_t F = uni[t];
+        if (F != 0) {
+            G = read_hdr_global(t0, tlen, 0, mode).adv;
+            off = F * G;
+            cnt = F;
+        }
+    }
     int par = 0;
     for (;;) {
         // ---- speculation step ----
@@ -201,16 +259,34 @@ hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64
     return hipGetLastError();
 }
 
+size_t tscan_uni_bytes(uint32_t ntables) { return (size_t)ntables * 8; }
+
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
-                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch) {
+                        bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
+                        void *uni_scratch) {
+    unsigned long long *uni = reinterpret_cast<unsigned long long *>(uni_scratch);
+    hipError_t e = hipMemsetAsync(uni, 0xff, tscan_uni_bytes(ntables), L.stream);
+    if (e != hipSuccess) return e;
+    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // gridDim.y <= 65535
+        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
+        hipLaunchKernelGGL((k_tscan_uni<false>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src, table_off + t0,
+                           mode, uni + t0, out, max_out, first + t0);
+    }
     hipLaunchKernelGGL((k_tscan<false>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end);
-    hipError_t e = hipGetLastError();
+                       max_out, first, out_end, uni);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = launch_exclusive_scan_u64(L, first, first, ntables, scan_scratch);
     if (e != hipSuccess) return e;
+    if (out != nullptr && max_out != 0) {
+        for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {
+            const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
+            hipLaunchKernelGGL((k_tscan_uni<true>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src,
+                               table_off + t0, mode, uni + t0, out, max_out, first + t0);
+        }
+    }
     hipLaunchKernelGGL((k_tscan<true>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end);
+                       max_out, first, out_end, uni);
     return hipGetLastError();
 }
 

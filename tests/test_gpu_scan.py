@@ -95,6 +95,31 @@ def test_uniform_tables(codec, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_uniform_prefix_edges(codec, mode):
+    """The grid-wide uniform-prefix pass (records i * G0 of the first record's length G0) hands
+    the walk over at the first record that differs: prefixes broken by one odd record and then
+    resumed at the same length (the resumed run is the walk's), a first record of another length,
+    a prefix of one record, a prefix ending in every stop rule, and a prefix long enough to span
+    many of the pass's 16,384-record strides."""
+    rng = random.Random(12)
+    k, v = rand_bytes(rng, 32), rand_bytes(rng, 1000)
+    run = lambda n: b"".join(rec(k, v, seq=i + 1) for i in range(n))
+    odd = rec(b"odd-one", rand_bytes(rng, 77))
+    tables = [
+        run(1000) + odd + run(500) + bytes(12),
+        odd + run(1000) + bytes(12),
+        run(1) + odd + run(3) + bytes(12),
+        run(2),
+        run(300) + rec(b"z", b"") + run(5) + bytes(12),               # valueSize 0 after the prefix
+        run(300) + struct.pack("<III", 0, 9, 1) + b"x" * 40,          # ikeySize 0
+        run(300) + struct.pack("<III", 4, 1 << 20, 1) + b"abcd",      # value past the end
+        run(300) + b"panic",                                          # short header
+        run(40000) + bytes(12),
+    ]
+    assert check(codec, tables, mode) > 42000
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_mixed_lengths_and_runs(codec, mode):
     rng = random.Random(2)
     tables = []
