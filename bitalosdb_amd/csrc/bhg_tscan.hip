@@ -11,9 +11,11 @@
 //    not G (or that hits a stop rule) are all true record starts, and that
 //    first different one is a true start too: up to 1025 records per
 //    global-memory round trip.
-//  * window chase (mixed lengths): the workgroup stages the next 64 KiB of
-//    the table in LDS with coalesced loads and thread 0 follows the headers
-//    at LDS latency.
+//  * window chase (mixed lengths): the workgroup stages the next 128 KiB of
+//    the table in LDS with coalesced loads (all in flight at once) and thread
+//    0 follows the headers at LDS latency.  Windows follow each other with no
+//    speculation step between them until the chase sees a run of 16 equal
+//    lengths.
 // The scan runs twice: count per table -> exclusive scan (out_first) ->
 // the same walk again writing the handles.
 //
@@ -33,7 +35,7 @@ namespace {
 
 constexpr int TS_THREADS = 1024;
 constexpr int TS_WAVES = TS_THREADS / 64;
-constexpr uint32_t TS_WIN = 64 * 1024;
+constexpr uint32_t TS_WIN = 128 * 1024;  // one workgroup per table and CU: most of the LDS
 
 struct Hdr {
     bool stop;
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
     __shared__ uint32_t s_brk[2][TS_WAVES];
     __shared__ uint64_t s_adv[2][TS_WAVES];
     __shared__ uint64_t s_off, s_cnt, s_G;
-    __shared__ int s_done;
+    __shared__ int s_done, s_chase;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t t = blockIdx.x;
@@ -139,7 +141,9 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
         }
     }
     int par = 0;
+    bool chase = false;  // the last window's lengths were mixed: the next step is a window again
     for (;;) {
+      if (!chase) {
         // ---- speculation step ----
         const uint64_t po = off + (uint64_t)tid * G;
         Hdr h = {true, 0};
@@ -173,21 +177,32 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
         off += adv_a;
         G = adv_a;
         if (a >= 32 || G_prev == 0) continue;  // speculation still pays (or had no guess yet)
+      }
 
         // ---- window chase: stage [off, off + TS_WIN) in LDS, thread 0 follows headers ----
         const uint64_t wbeg = off;
         const uint64_t wend = tlen > off ? (tlen - off < TS_WIN ? tlen : off + TS_WIN) : off;
         const uint32_t wlen = (uint32_t)(wend - wbeg);
-        for (uint32_t b = tid * 16; b < wlen; b += TS_THREADS * 16) {
-            if (b + 16 <= wlen) {
-                *reinterpret_cast<u32x4_a4 *>(win + b) = gld<u32x4_a4>(t0 + wbeg + b);
-            } else {
-                for (uint32_t j = b; j < wlen; j++) win[j] = gld<uint8_t>(t0 + wbeg + j);
+        if (wlen == TS_WIN) {  // a whole window: every load in flight before the first store
+            constexpr uint32_t PER = TS_WIN / (TS_THREADS * 16);
+            u32x4 r[PER];
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) r[q] = gld<u32x4_a4>(t0 + wbeg + 16 * (q * TS_THREADS + tid));
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) *reinterpret_cast<u32x4_a4 *>(win + 16 * (q * TS_THREADS + tid)) = r[q];
+        } else {
+            for (uint32_t b = tid * 16; b < wlen; b += TS_THREADS * 16) {
+                if (b + 16 <= wlen) {
+                    *reinterpret_cast<u32x4_a4 *>(win + b) = gld<u32x4_a4>(t0 + wbeg + b);
+                } else {
+                    for (uint32_t j = b; j < wlen; j++) win[j] = gld<uint8_t>(t0 + wbeg + j);
+                }
             }
         }
         __syncthreads();
         if (tid == 0) {
             int done = 0;
+            uint32_t run = 0;  // records in a row of the same length
             for (;;) {
                 const uint64_t rem = tlen > off ? tlen - off : 0;
                 if (rem < 12) { done = 1; break; }
@@ -198,17 +213,20 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
                 if (WRITE && w0 + cnt < max_out) out[w0 + cnt] = bhg_handle{tbase + off, (uint32_t)hh.adv, 0};
                 cnt += 1;
                 off += hh.adv;
+                run = hh.adv == G ? run + 1 : 0;
                 G = hh.adv;
             }
             s_off = off;
             s_cnt = cnt;
             s_G = G;
             s_done = done;
+            s_chase = run < 16;
         }
         __syncthreads();
         off = s_off;
         cnt = s_cnt;
         G = s_G;
+        chase = s_chase != 0;
         if (s_done) break;
         // the next chase overwrites win / s_*: every reader passes the speculation barrier first
     }
