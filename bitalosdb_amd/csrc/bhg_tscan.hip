@@ -26,6 +26,12 @@
 // bulk-loaded table is one uniform prefix ended by its terminating stop, so the
 // one-workgroup walk only starts at record F; the F handles are written by a
 // grid-wide pass (k_tscan_uni<true>).
+//
+// The count walk logs its steps (start offset, record count, and for a
+// speculation step its guess, run and break record); the write pass then
+// replays every logged step at once, a wave per step (k_tscan_logw: a window is
+// re-chased from global memory by one lane), instead of walking each table
+// again.  A table with more than TS_LOG_CAP steps is written by the serial walk.
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -36,6 +42,15 @@ namespace {
 constexpr int TS_THREADS = 1024;
 constexpr int TS_WAVES = TS_THREADS / 64;
 constexpr uint32_t TS_WIN = 128 * 1024;  // one workgroup per table and CU: most of the LDS
+constexpr uint32_t TS_LOG_CAP = 4096;     // logged walk steps per table (128 KiB)
+
+// one step of the count walk: a speculation step found `a` records of length G at off + i G
+// (x = a << 32, plus bit 62 and the u32 length when record a followed with another length), or a
+// window chase started at off (x bit 63)
+struct TsLog {
+    uint64_t off, cnt, G, x;
+};
+constexpr uint64_t TS_LOG_WIN = 1ull << 63, TS_LOG_BRK = 1ull << 62;
 
 struct Hdr {
     bool stop;
@@ -118,7 +133,10 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
                                                       const uint64_t *__restrict__ table_off, int mode,
                                                       bhg_handle *__restrict__ out, uint64_t max_out,
                                                       uint64_t *__restrict__ first, uint64_t *__restrict__ out_end,
-                                                      const unsigned long long *__restrict__ uni) {
+                                                      const unsigned long long *__restrict__ uni,
+                                                      TsLog *__restrict__ logs, uint32_t *__restrict__ log_n) {
+    // WRITE: only the tables whose walk overflowed the log (the others are replayed by k_tscan_logw)
+    if (WRITE && log_n[blockIdx.x] <= TS_LOG_CAP) return;
     __shared__ alignas(16) uint8_t win[TS_WIN];
     __shared__ uint32_t s_brk[2][TS_WAVES];
     __shared__ uint64_t s_adv[2][TS_WAVES];
@@ -142,6 +160,13 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
     }
     int par = 0;
     bool chase = false;  // the last window's lengths were mixed: the next step is a window again
+    uint32_t nlog = 0;   // count walk: steps logged (the same on every thread)
+    auto log_step = [&](uint64_t o, uint64_t c, uint64_t g, uint64_t x) {
+        if (!WRITE) {
+            if (tid == 0 && nlog < TS_LOG_CAP) logs[(uint64_t)t * TS_LOG_CAP + nlog] = TsLog{o, c, g, x};
+            nlog++;
+        }
+    };
     for (;;) {
       if (!chase) {
         // ---- speculation step ----
@@ -165,6 +190,8 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
             }
         }
         par ^= 1;  // the next step writes the other slot: no second barrier needed
+        log_step(off, cnt, G, ((uint64_t)a << 32) |
+                                  (a < TS_THREADS && adv_a != ~0ull ? TS_LOG_BRK | (uint32_t)adv_a : 0ull));
         if (WRITE && tid < a && w0 + cnt + tid < max_out)
             out[w0 + cnt + tid] = bhg_handle{tbase + po, (uint32_t)G, 0};
         cnt += a;
@@ -183,6 +210,7 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
         const uint64_t wbeg = off;
         const uint64_t wend = tlen > off ? (tlen - off < TS_WIN ? tlen : off + TS_WIN) : off;
         const uint32_t wlen = (uint32_t)(wend - wbeg);
+        log_step(wbeg, cnt, 0, TS_LOG_WIN);
         if (wlen == TS_WIN) {  // a whole window: every load in flight before the first store
             constexpr uint32_t PER = TS_WIN / (TS_THREADS * 16);
             u32x4 r[PER];
@@ -231,8 +259,50 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
         // the next chase overwrites win / s_*: every reader passes the speculation barrier first
     }
     if (tid == 0) {
-        if (!WRITE) first[t] = cnt;
-        else if (out_end) out_end[t] = off;
+        if (!WRITE) {
+            first[t] = cnt;
+            log_n[t] = nlog;
+        }
+        if (out_end) out_end[t] = off;
+    }
+}
+
+// the write pass of the logged walks: one wave per logged step, handles at out[first[t] + cnt ...]
+constexpr int TL_THREADS = 256, TL_PARTS = 64;  // workgroups per table
+__global__ __launch_bounds__(TL_THREADS) void k_tscan_logw(const uint8_t *__restrict__ src,
+                                                           const uint64_t *__restrict__ table_off, int mode,
+                                                           bhg_handle *__restrict__ out, uint64_t max_out,
+                                                           const uint64_t *__restrict__ first,
+                                                           const TsLog *__restrict__ logs,
+                                                           const uint32_t *__restrict__ log_n) {
+    const uint32_t t = blockIdx.y, lane = threadIdx.x & 63;
+    const uint32_t n = log_n[t];
+    if (n > TS_LOG_CAP) return;  // written by the serial walk
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase, tend = t0 + tlen;
+    const uint64_t w0 = first[t];
+    constexpr uint32_t WPT = TL_PARTS * (TL_THREADS / 64);
+    for (uint32_t k = blockIdx.x * (TL_THREADS / 64) + (threadIdx.x >> 6); k < n; k += WPT) {
+        const TsLog e = logs[(uint64_t)t * TS_LOG_CAP + k];
+        if (!(e.x & TS_LOG_WIN)) {  // speculation step: a records of length G, then maybe record a
+            const uint32_t a = (uint32_t)(e.x >> 32) & 0x7ffu;
+            for (uint32_t i = lane; i < a; i += 64)
+                if (w0 + e.cnt + i < max_out) out[w0 + e.cnt + i] = bhg_handle{tbase + e.off + i * e.G, (uint32_t)e.G, 0};
+            if ((e.x & TS_LOG_BRK) && lane == 0 && w0 + e.cnt + a < max_out)
+                out[w0 + e.cnt + a] = bhg_handle{tbase + e.off + (uint64_t)a * e.G, (uint32_t)e.x, 0};
+        } else if (lane == 0) {  // window: the count walk's chase, from global memory
+            uint64_t off = e.off, cnt = e.cnt;
+            const uint64_t wend = tlen > off ? (tlen - off < TS_WIN ? tlen : off + TS_WIN) : off;
+            for (;;) {
+                const uint64_t rem = tlen > off ? tlen - off : 0;
+                if (rem < 12 || off + 8 > wend) break;
+                const Hdr hh = hdr_rule(rem, ldu32(t0 + off, tend), ldu32(t0 + off + 4, tend), mode);
+                if (hh.stop) break;
+                if (w0 + cnt < max_out) out[w0 + cnt] = bhg_handle{tbase + off, (uint32_t)hh.adv, 0};
+                cnt += 1;
+                off += hh.adv;
+            }
+        }
     }
 }
 
@@ -277,12 +347,16 @@ hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64
     return hipGetLastError();
 }
 
-size_t tscan_uni_bytes(uint32_t ntables) { return (size_t)ntables * 8; }
+size_t tscan_uni_bytes(uint32_t ntables) {
+    return (size_t)ntables * 8 + (((size_t)ntables * 4 + 255) & ~(size_t)255) + (size_t)ntables * TS_LOG_CAP * sizeof(TsLog);
+}
 
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                         bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
                         void *uni_scratch) {
     unsigned long long *uni = reinterpret_cast<unsigned long long *>(uni_scratch);
+    uint32_t *log_n = reinterpret_cast<uint32_t *>(uni + ntables);
+    TsLog *logs = reinterpret_cast<TsLog *>(reinterpret_cast<uint8_t *>(log_n) + (((size_t)ntables * 4 + 255) & ~(size_t)255));
     hipError_t e = hipMemsetAsync(uni, 0xff, tscan_uni_bytes(ntables), L.stream);
     if (e != hipSuccess) return e;
     for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // gridDim.y <= 65535
@@ -291,20 +365,21 @@ hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *tab
                            mode, uni + t0, out, max_out, first + t0);
     }
     hipLaunchKernelGGL((k_tscan<false>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end, uni);
+                       max_out, first, out_end, uni, logs, log_n);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = launch_exclusive_scan_u64(L, first, first, ntables, scan_scratch);
     if (e != hipSuccess) return e;
-    if (out != nullptr && max_out != 0) {
-        for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {
-            const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
-            hipLaunchKernelGGL((k_tscan_uni<true>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src,
-                               table_off + t0, mode, uni + t0, out, max_out, first + t0);
-        }
+    if (out == nullptr || max_out == 0) return hipGetLastError();  // counts and ends only
+    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {
+        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
+        hipLaunchKernelGGL((k_tscan_uni<true>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src,
+                           table_off + t0, mode, uni + t0, out, max_out, first + t0);
+        hipLaunchKernelGGL(k_tscan_logw, dim3(TL_PARTS, m), dim3(TL_THREADS), 0, L.stream, src, table_off + t0, mode,
+                           out, max_out, first + t0, logs + (size_t)t0 * TS_LOG_CAP, log_n + t0);
     }
     hipLaunchKernelGGL((k_tscan<true>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end, uni);
+                       max_out, first, out_end, uni, logs, log_n);
     return hipGetLastError();
 }
 
