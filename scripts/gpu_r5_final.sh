@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 5 closing measurements on the committed tree, in two parts (one gpurun call each):
 #   PART=a: GPU tests, smoke, the driver-shaped C2 line, C2 kernel stats, C2 SQ counters
-#   PART=b: C3 / C4 / C5-snappy / mixdec / Get / tail / indexcrc lines, kernel stats, C3 + C4 SQ counters, gloo x2
+#   PART=b: C3 / C4 / C5-snappy / mixdec / Get / tail / indexcrc / scan / scanmix lines, kernel stats, the
+#           one-rank RCCL rehearsal of the N > 1 line, C3 + C4 SQ counters, gloo x2
 #   PART=c: part b from the tail line on
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -38,6 +39,9 @@ else
   line get --config get --warmup 5; } &&
   line tail --config tail --warmup 5 &&
   line indexcrc --config indexcrc --warmup 5 &&
+  line scan --config scan --warmup 5 &&
+  line scanmix --config scanmix --warmup 2 --steps 5 &&
+  { export BHG_BENCH_PG1=1; line pg1_nccl --steps 5 --warmup 2; r=$?; unset BHG_BENCH_PG1; [ $r = 0 ]; } &&
   line g2_gloo --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu --no-e2e --no-c5 &&
   ARGS="--config c3 --no-secondary" TAG=final/pmc_c3 KERNEL=k_ bash scripts/pmc_bench.sh &&
   ARGS="--config c4 --no-secondary" TAG=final/pmc_c4 KERNEL=k_snappy_enc bash scripts/pmc_bench.sh
