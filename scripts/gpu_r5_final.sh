@@ -3,7 +3,7 @@
 #   PART=a: GPU tests, smoke, the driver-shaped C2 line, C2 kernel stats, C2 SQ counters
 #   PART=b: C3 / C4 / C5-snappy / mixdec / Get / tail / indexcrc / scan / scanmix lines, kernel stats, the
 #           one-rank RCCL rehearsal of the N > 1 line, C3 + C4 SQ counters, gloo x2
-#   PART=c: part b from the tail line on
+#   PART=c: part b from the tail line on; PART=d: from the RCCL rehearsal line on
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -17,7 +17,7 @@ stats() {  # stats <name> <bench args...>: rocprofv3 kernel stats of one bench l
 line() {  # line <name> <bench args...>
   local nm=$1; shift
   timeout -k 10 500 python3 -u bench.py "$@" > $O/bench_$nm.json 2> $O/bench_$nm.err || { tail -20 $O/bench_$nm.err; return 1; }
-  python3 -c "import json; d=json.load(open('$O/bench_$nm.json')); print('$nm', d['value'], d['unit'], d.get('ms_per_step'), d.get('roofline', {}).get('frac'))"
+  python3 -c "import json; d=json.loads(open('$O/bench_$nm.json').read().strip().splitlines()[-1]); print('$nm', d['value'], d['unit'], d.get('ms_per_step'), d.get('roofline', {}).get('frac'))"
 }
 if [ "$PART" = a ]; then
   timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
@@ -28,7 +28,7 @@ if [ "$PART" = a ]; then
   stats c2 --warmup 5 --no-cpu --no-e2e --no-traffic --no-c5 &&
   ARGS="--warmup 5" TAG=final/pmc_c2 KERNEL=k_decode_tile bash scripts/pmc_bench.sh
 else
-  [ "$PART" = c ] || {
+  [ "$PART" = c ] || [ "$PART" = d ] || {
   line c3 --config c3 --warmup 5 &&
   stats c3 --config c3 --warmup 5 --no-cpu --no-e2e --no-secondary &&
   line c4 --config c4 --warmup 5 &&
@@ -37,10 +37,11 @@ else
   line mixdec --config mixdec --steps 10 --warmup 5 &&
   stats mixdec --config mixdec --steps 10 --warmup 5 &&
   line get --config get --warmup 5; } &&
+  { [ "$PART" = d ] || {
   line tail --config tail --warmup 5 &&
   line indexcrc --config indexcrc --warmup 5 &&
   line scan --config scan --warmup 5 &&
-  line scanmix --config scanmix --warmup 2 --steps 5 &&
+  line scanmix --config scanmix --warmup 2 --steps 5; }; } &&
   { export BHG_BENCH_PG1=1; line pg1_nccl --steps 5 --warmup 2; r=$?; unset BHG_BENCH_PG1; [ $r = 0 ]; } &&
   line g2_gloo --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu --no-e2e --no-c5 &&
   ARGS="--config c3 --no-secondary" TAG=final/pmc_c3 KERNEL=k_ bash scripts/pmc_bench.sh &&
