@@ -119,6 +119,22 @@ def test_uniform_prefix_edges(codec, mode):
     assert check(codec, tables, mode) > 42000
 
 
+def test_step_log_overflow_falls_back_to_the_serial_walk(codec):
+    """The write pass replays the count walk's logged steps (k_tscan_logw); a table whose walk
+    takes more than TS_LOG_CAP = 4,096 steps (here ~4,300 windows of 128 KiB: a 540-MB table of
+    mixed lengths after a uniform prefix) is written by the serial walk instead.  Beside it, a
+    small mixed table takes the replay; both must match the restatement."""
+    rng = random.Random(13)
+    chunk = b"".join(rec(rand_bytes(rng, rng.randrange(8, 40)), rand_bytes(rng, rng.randrange(100, 4000)), seq=i + 1)
+                     for i in range(500))
+    k, v = rand_bytes(rng, 32), rand_bytes(rng, 1000)
+    prefix = b"".join(rec(k, v, seq=i + 1) for i in range(3000))
+    reps = (540 << 20) // len(chunk) + 1
+    big = prefix + chunk * reps + bytes(12)
+    small = chunk * 3 + bytes(12)
+    assert check(codec, [big, small], 0) > 500 * reps
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_mixed_lengths_and_runs(codec, mode):
     rng = random.Random(2)
