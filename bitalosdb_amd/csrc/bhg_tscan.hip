@@ -112,8 +112,9 @@ __global__ __launch_bounds__(TU_THREADS) void k_tscan_uni(const uint8_t *__restr
         if (i0 == 0) atomicMin(uni + t, 0ull);
         return;
     }
-    // record tlen / G cannot have length G (it would end past the table), so F <= tlen / G
-    const uint64_t last = tlen / G;
+    // record tlen / G + 1 starts past the table's end and stops, so F <= tlen / G + 1 (in mode 1 a
+    // record of length G may start at tlen / G: its value may run past the end, writer.go:566-572)
+    const uint64_t last = tlen / G + 1;
     for (uint64_t i = i0; i - lane <= last; i += step) {  // whole waves iterate together
         bool bad = false;
         if (i <= last) {

@@ -115,6 +115,8 @@ def test_uniform_prefix_edges(codec, mode):
         run(300) + struct.pack("<III", 4, 1 << 20, 1) + b"abcd",      # value past the end
         run(300) + b"panic",                                          # short header
         run(40000) + bytes(12),
+        run(6)[:-100],                                                # the last record's value cut short
+        struct.pack("<III", 4, 1 << 20, 1) + b"abcd",                 # record 0 runs past the end
     ]
     assert check(codec, tables, mode) > 42000
 
