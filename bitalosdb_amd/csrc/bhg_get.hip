@@ -66,13 +66,19 @@ constexpr uint32_t kItemOff = kHdr + kShards * 4;
 constexpr uint32_t kItem = 10;               // HashIndexItem64Size
 constexpr uint64_t kSearchTrailer = ((1ull << 56) - 1) << 8 | 18;  // MakeSearchKey: SeqNumMax, KindMax
 
+// big-endian fields of the index by dword loads (ldu32: two aligned dwords + v_alignbyte, bytes
+// only past `end`): the byte loads they replace made k_get memory-instruction bound
+__device__ __forceinline__ uint32_t be32w(uint64_t a, uint64_t end) { return __builtin_bswap32(ldu32(a, end)); }
+__device__ __forceinline__ uint32_t be16w(uint64_t a, uint64_t end) { return be32w(a, end) >> 16; }
+
 // HashIndex.Get64 (hash_index.go:399-431); false = not found
 __device__ bool get64(uint64_t d, uint64_t len, uint32_t key, uint64_t &val) {
     if (len <= kItemOff) return false;        // SetReader rejects len(d) <= itemOffset
-    if (be32(d + 4) == 0) return false;       // header.shards <= 0
+    const uint64_t end = d + len;
+    if (be32w(d + 4, end) == 0) return false;  // header.shards <= 0
     const uint32_t hid = key >> 16, lid = key & 0xffffu;
-    const uint32_t origin = hid > 0 ? be32(d + kHdr + (hid - 1) * 4) : 0u;
-    const uint32_t dest = be32(d + kHdr + hid * 4);
+    const uint32_t origin = hid > 0 ? be32w(d + kHdr + (hid - 1) * 4, end) : 0u;
+    const uint32_t dest = be32w(d + kHdr + hid * 4, end);
     if (dest <= origin) return false;
     const uint32_t cnt = dest - origin;
     const uint64_t cur = d + kItemOff + (uint64_t)origin * kItem;
@@ -80,11 +86,12 @@ __device__ bool get64(uint64_t d, uint64_t len, uint32_t key, uint64_t &val) {
     uint32_t i = 0, j = cnt;
     while (i < j) {
         const uint32_t h = (i + j) >> 1;
-        if (be16(cur + (uint64_t)kItem * h) < lid) i = h + 1;
+        if (be16w(cur + (uint64_t)kItem * h, end) < lid) i = h + 1;
         else j = h;
     }
-    if (i < cnt && be16(cur + (uint64_t)kItem * i) == lid) {
-        val = be64(cur + (uint64_t)kItem * i + 2);
+    if (i < cnt && be16w(cur + (uint64_t)kItem * i, end) == lid) {
+        const uint64_t a = cur + (uint64_t)kItem * i + 2;
+        val = ((uint64_t)be32w(a, end) << 32) | be32w(a + 4, end);
         return true;
     }
     return false;
@@ -192,9 +199,27 @@ __device__ __forceinline__ uint32_t table_lookup(uint64_t base, uint64_t src_len
     return BHG_ST_OK;
 }
 
+// hash.Fnv32 of the query key, its bytes loaded a dword at a time
 __device__ __forceinline__ uint32_t query_hash(uint64_t kp, uint32_t klen) {
     uint32_t kh = BHG_FNV_OFFSET;
-    for (uint32_t b = 0; b < klen; b++) kh = (kh * BHG_FNV_PRIME) ^ ld8(kp + b);
+    const uint64_t kend = kp + klen;
+    uint32_t q = 0;
+    for (; q + 16 <= klen; q += 16) {  // four dwords in flight
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) w[u] = ldu32(kp + q + 4 * u, kend);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) kh = (kh * BHG_FNV_PRIME) ^ ((w[u] >> (8 * b)) & 0xffu);
+    }
+    for (; q < klen; q += 4) {
+        const uint32_t w = ldu32(kp + q, kend);  // bytes past kend read as 0 and not hashed
+        const uint32_t nb = klen - q < 4 ? klen - q : 4u;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; b++)
+            if (b < nb) kh = (kh * BHG_FNV_PRIME) ^ ((w >> (8 * b)) & 0xffu);
+    }
     return kh;
 }
 
