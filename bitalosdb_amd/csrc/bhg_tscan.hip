@@ -137,7 +137,10 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan(const uint8_t *__restrict_
                                                       const unsigned long long *__restrict__ uni,
                                                       TsLog *__restrict__ logs, uint32_t *__restrict__ log_n) {
     // WRITE: only the tables whose walk overflowed the log (the others are replayed by k_tscan_logw)
-    if (WRITE && log_n[blockIdx.x] <= TS_LOG_CAP) return;
+    // count: not the tables the segment walks resolved (log_n = ~0); write: only the tables whose
+    // serial walk overflowed the log (the others are replayed by k_tscan_logw / k_tscan_segw)
+    if (!WRITE && log_n[blockIdx.x] == ~0u) return;
+    if (WRITE && (log_n[blockIdx.x] <= TS_LOG_CAP || log_n[blockIdx.x] == ~0u)) return;
     __shared__ alignas(16) uint8_t win[TS_WIN];
     __shared__ uint32_t s_brk[2][TS_WAVES];
     __shared__ uint64_t s_adv[2][TS_WAVES];
@@ -307,6 +310,263 @@ __global__ __launch_bounds__(TL_THREADS) void k_tscan_logw(const uint8_t *__rest
     }
 }
 
+// ---- speculative segment walks (mixed lengths) ----
+// After the uniform prefix (end P) a table's region [P, tlen) is cut into TS_SEGS segments.
+// k_tscan_seg: segment j's workgroup guesses where the record chain enters it (j = 0: P itself;
+// else the first of its first 64 KiB of positions whose chain survives TS_SURVIVE headers inside
+// the staged 128-KiB window, or ends there in a terminator or exactly at the data's end), walks the chain from there to the first node at or past the segment's end, and logs its
+// windows.  k_tscan_stitch then follows the true chain: where it enters segment j at e, e must
+// be a node of that walk (re-chased from the logged window holding e), and the walk's records
+// from e on are the table's.  A miss (no guess, a wrong guess, a log overflow) sends the table
+// to the serial walk (k_tscan), so a guess never decides a result.
+constexpr uint32_t TS_SEGS = 64, TS_SEG_LOG = 256, TS_PROBE = 64 * 1024, TS_SURVIVE = 8;
+constexpr uint64_t TS_SEG_MIN = 1ull << 20;
+struct TsSeg {
+    uint64_t g, cnt, x;  // guessed entry; records walked in [g, segment end); where the walk stopped
+    uint32_t nlog, flags;
+    uint64_t base, r;    // (stitch) out index of the walk's record 0 within the table; first record used
+};
+constexpr uint32_t TSF_WALKED = 1, TSF_END = 2, TSF_FAIL = 4;
+struct TsWin {
+    uint64_t off, cnt, we;  // a logged window: chase start, records before it, staged window end
+};
+
+__device__ __forceinline__ uint64_t prefix_end(uint64_t t0, uint64_t tlen, int mode, uint64_t F) {
+    return F ? F * read_hdr_global(t0, tlen, 0, mode).adv : 0ull;
+}
+__device__ __forceinline__ void seg_geo(uint64_t P, uint64_t tlen, uint32_t j, uint64_t &s0, uint64_t &s1) {
+    const uint64_t span = tlen > P ? tlen - P : 0;
+    uint64_t S = (span + TS_SEGS - 1) / TS_SEGS;
+    if (S < TS_SEG_MIN) S = TS_SEG_MIN;
+    s0 = P + (uint64_t)j * S;
+    s1 = s0 + S;
+    if (s0 > tlen) s0 = tlen;
+    if (s1 > tlen || j == TS_SEGS - 1) s1 = tlen;
+}
+// one step of the chase inside a window: the shared rules of the walk, its log replay and the
+// stitch's membership check.  0: record (adv), 1: at / past the segment end, 2: table end or stop,
+// 3: header not inside the window
+__device__ __forceinline__ int seg_step(uint64_t off, uint64_t s1, uint64_t tlen, uint64_t we, uint32_t k, uint32_t v,
+                                        int mode, uint64_t &adv) {
+    if (off >= s1) return 1;
+    const uint64_t rem = tlen > off ? tlen - off : 0;
+    if (rem < 12) return 2;
+    if (off + 8 > we) return 3;
+    const Hdr hh = hdr_rule(rem, k, v, mode);
+    if (hh.stop) return 2;
+    adv = hh.adv;
+    return 0;
+}
+
+__global__ __launch_bounds__(TS_THREADS) void k_tscan_seg(const uint8_t *__restrict__ src,
+                                                          const uint64_t *__restrict__ table_off, int mode,
+                                                          const unsigned long long *__restrict__ uni,
+                                                          TsSeg *__restrict__ segs, TsWin *__restrict__ wins) {
+    __shared__ alignas(16) uint8_t win[TS_WIN];
+    __shared__ uint32_t s_best, s_nlog;
+    __shared__ uint64_t s_off, s_cnt;
+    __shared__ int s_state;
+    const uint32_t tid = threadIdx.x, j = blockIdx.x, t = blockIdx.y;
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase;
+    const uint64_t P = prefix_end(t0, tlen, mode, uni[t]);
+    uint64_t s0, s1;
+    seg_geo(P, tlen, j, s0, s1);
+    TsSeg *sg = segs + (uint64_t)t * TS_SEGS + j;
+    TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
+    if (s0 >= s1) {
+        if (tid == 0) *sg = TsSeg{s0, 0, s0, 0, 0, 0, ~0ull};
+        return;
+    }
+    auto stage = [&](uint64_t wbeg) -> uint64_t {  // [wbeg, we) into LDS; returns we
+        const uint64_t we = tlen - wbeg < TS_WIN ? tlen : wbeg + TS_WIN;
+        const uint32_t wlen = (uint32_t)(we - wbeg);
+        if (wlen == TS_WIN) {
+            constexpr uint32_t PER = TS_WIN / (TS_THREADS * 16);
+            u32x4 r[PER];
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) r[q] = gld<u32x4_a4>(t0 + wbeg + 16 * (q * TS_THREADS + tid));
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) *reinterpret_cast<u32x4_a4 *>(win + 16 * (q * TS_THREADS + tid)) = r[q];
+        } else {
+            for (uint32_t b = tid * 16; b < wlen; b += TS_THREADS * 16) {
+                if (b + 16 <= wlen) *reinterpret_cast<u32x4_a4 *>(win + b) = gld<u32x4_a4>(t0 + wbeg + b);
+                else for (uint32_t q = b; q < wlen; q++) win[q] = gld<uint8_t>(t0 + wbeg + q);
+            }
+        }
+        return we;
+    };
+    auto hdr_lds = [&](uint64_t off, uint64_t wb, uint32_t &k, uint32_t &v) {
+        const uint8_t *h = win + (off - wb);
+        k = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+        v = (uint32_t)h[4] | ((uint32_t)h[5] << 8) | ((uint32_t)h[6] << 16) | ((uint32_t)h[7] << 24);
+    };
+    uint64_t wb = s0, we = stage(s0);
+    if (tid == 0) s_best = j == 0 ? 0u : ~0u;
+    __syncthreads();
+    if (j > 0) {  // the guess: the first probed position whose chain survives TS_SURVIVE headers
+        const uint64_t lim = s1 - s0 < TS_PROBE ? s1 - s0 : TS_PROBE;
+        for (uint32_t c = tid; c < lim; c += TS_THREADS) {
+            uint64_t q = s0 + c;
+            uint32_t n = 0;
+            bool acc = false;
+            for (;;) {
+                // the data's end after a record: landing inside the table's last 12 bytes (a false
+                // chain's jump past the end -- a rebuild-mode value running out -- does not count)
+                if (q > tlen) break;
+                const uint64_t rem = tlen - q;
+                if (rem < 12) { acc = n > 0; break; }
+                // a chain that leaves the staged window is not taken: false headers jump anywhere
+                // up to 4 GB, and one landing on a true record later merges with the true chain
+                // (measured: 3 of 16 scanmix tables missed); 8 true records of <= 4 KiB stay inside
+                if (q + 8 > we) break;
+                uint32_t k, v;
+                hdr_lds(q, wb, k, v);
+                const Hdr hh = hdr_rule(rem, k, v, mode);
+                if (hh.stop) { acc = n > 0 && k == 0 && v == 0; break; }  // a terminator after a record
+                if (++n == TS_SURVIVE) { acc = true; break; }
+                q += hh.adv;
+            }
+            if (acc) {
+                atomicMin(&s_best, c);
+                break;  // this thread's later positions are larger
+            }
+        }
+        __syncthreads();
+    }
+    if (s_best == ~0u) {
+        if (tid == 0) *sg = TsSeg{s0, 0, s0, 0, TSF_FAIL, 0, ~0ull};
+        return;
+    }
+    const uint64_t g = s0 + s_best;
+    uint64_t off = g, cnt = 0;
+    uint32_t nlog = 0;
+    int state = 0;
+    for (;;) {
+        if (tid == 0) {  // chase inside the staged window
+            if (nlog < TS_SEG_LOG) wl[nlog] = TsWin{off, cnt, we};
+            nlog++;
+            for (;;) {
+                uint32_t k = 0, v = 0;
+                if (off < s1 && off + 8 <= we && off + 12 <= tlen) hdr_lds(off, wb, k, v);
+                uint64_t adv = 0;
+                const int r = seg_step(off, s1, tlen, we, k, v, mode, adv);
+                if (r == 3) break;
+                if (r != 0) { state = r; break; }
+                cnt++;
+                off += adv;
+            }
+            s_off = off;
+            s_cnt = cnt;
+            s_nlog = nlog;
+            s_state = state;
+        }
+        __syncthreads();
+        off = s_off;
+        cnt = s_cnt;
+        nlog = s_nlog;
+        state = s_state;
+        if (state != 0) break;
+        wb = off;
+        we = stage(wb);
+        __syncthreads();
+    }
+    if (tid == 0)
+        *sg = TsSeg{g, cnt, off, nlog, TSF_WALKED | (state == 2 ? TSF_END : 0u) | (nlog > TS_SEG_LOG ? TSF_FAIL : 0u), 0,
+                    ~0ull};  // r: set by the stitch for the segments the chain uses
+}
+
+// one lane per table: follow the true chain through the segment walks (see above)
+__global__ __launch_bounds__(64) void k_tscan_stitch(const uint8_t *__restrict__ src,
+                                                     const uint64_t *__restrict__ table_off, int mode,
+                                                     const unsigned long long *__restrict__ uni,
+                                                     TsSeg *__restrict__ segs, const TsWin *__restrict__ wins,
+                                                     uint64_t *__restrict__ first, uint64_t *__restrict__ out_end,
+                                                     uint32_t *__restrict__ log_n) {
+    if (threadIdx.x != 0) return;
+    const uint32_t t = blockIdx.x;
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase, tend = t0 + tlen;
+    const uint64_t F = uni[t];
+    const uint64_t P = prefix_end(t0, tlen, mode, F);
+    uint64_t e = P, cnt = F;
+    bool ok = true;
+    for (uint32_t j = 0; j < TS_SEGS && ok; j++) {
+        uint64_t s0, s1;
+        seg_geo(P, tlen, j, s0, s1);
+        if (s0 >= s1) break;
+        TsSeg &sg = segs[(uint64_t)t * TS_SEGS + j];
+        if (e >= s1) continue;  // the chain jumped over this segment (r stays ~0: nothing written)
+        if (!(sg.flags & TSF_WALKED) || (sg.flags & TSF_FAIL) || e < sg.g) { ok = false; break; }
+        // the logged window holding e: the last one starting at or before e
+        const TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
+        uint32_t lo = 0, hi = sg.nlog;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (wl[mid].off <= e) lo = mid; else hi = mid;
+        }
+        uint64_t off = wl[lo].off, c = wl[lo].cnt;
+        const uint64_t we = wl[lo].we;
+        while (off < e) {
+            uint64_t adv = 0;
+            uint32_t k = 0, v = 0;
+            if (off + 12 <= tlen) { k = ldu32(t0 + off, tend); v = ldu32(t0 + off + 4, tend); }
+            if (seg_step(off, s1, tlen, we, k, v, mode, adv) != 0) break;
+            off += adv;
+            c++;
+        }
+        if (off != e) { ok = false; break; }
+        sg.r = c;
+        sg.base = cnt - c;
+        cnt += sg.cnt - c;
+        e = sg.x;
+        if (sg.flags & TSF_END) break;
+    }
+    if (ok) {
+        first[t] = cnt;
+        if (out_end) out_end[t] = e;
+        log_n[t] = ~0u;
+    } else {
+        log_n[t] = 0;  // the serial walk counts this table
+    }
+}
+
+// the write pass of the segment walks: one wave per logged window, records from the stitch's r on
+__global__ __launch_bounds__(TS_THREADS) void k_tscan_segw(const uint8_t *__restrict__ src,
+                                                           const uint64_t *__restrict__ table_off, int mode,
+                                                           const unsigned long long *__restrict__ uni,
+                                                           const TsSeg *__restrict__ segs, const TsWin *__restrict__ wins,
+                                                           const uint32_t *__restrict__ log_n,
+                                                           const uint64_t *__restrict__ first,
+                                                           bhg_handle *__restrict__ out, uint64_t max_out) {
+    const uint32_t j = blockIdx.x, t = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (log_n[t] != ~0u) return;
+    const TsSeg sg = segs[(uint64_t)t * TS_SEGS + j];
+    if (!(sg.flags & TSF_WALKED) || sg.r == ~0ull) return;
+    const uint64_t tbase = table_off[t], tlen = table_off[t + 1] - tbase;
+    const uint64_t t0 = (uint64_t)src + tbase, tend = t0 + tlen;
+    const uint64_t P = prefix_end(t0, tlen, mode, uni[t]);
+    uint64_t s0, s1;
+    seg_geo(P, tlen, j, s0, s1);
+    const TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
+    const uint64_t w0 = first[t] + sg.base;
+    const uint32_t nl = sg.nlog;
+    for (uint32_t q = wv; q < nl; q += TS_WAVES) {
+        if (lane != 0) continue;
+        const TsWin w = wl[q];
+        uint64_t off = w.off, c = w.cnt;
+        for (;;) {
+            uint32_t k = 0, v = 0;
+            if (off + 12 <= tlen) { k = ldu32(t0 + off, tend); v = ldu32(t0 + off + 4, tend); }
+            uint64_t adv = 0;
+            if (seg_step(off, s1, tlen, w.we, k, v, mode, adv) != 0) break;
+            if (c >= sg.r && w0 + c < max_out) out[w0 + c] = bhg_handle{tbase + off, (uint32_t)adv, 0};
+            off += adv;
+            c++;
+        }
+    }
+}
+
 // Writer.rebuild's per-record work after the header chase (writer.go:569-575):
 // bh = {offset inside the table, recordLen}, khash = hash.Fnv32(UserKey) of
 // base.DecodeInternalKey(key) (UserKey empty when ikeySize < 8), table index.
@@ -348,16 +608,25 @@ hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64
     return hipGetLastError();
 }
 
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t tscan_uni_bytes(uint32_t ntables) {
-    return (size_t)ntables * 8 + (((size_t)ntables * 4 + 255) & ~(size_t)255) + (size_t)ntables * TS_LOG_CAP * sizeof(TsLog);
+    return al256((size_t)ntables * 8) + al256((size_t)ntables * 4) + al256((size_t)ntables * TS_LOG_CAP * sizeof(TsLog)) +
+           al256((size_t)ntables * TS_SEGS * sizeof(TsSeg)) + (size_t)ntables * TS_SEGS * TS_SEG_LOG * sizeof(TsWin);
 }
 
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                         bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
                         void *uni_scratch) {
-    unsigned long long *uni = reinterpret_cast<unsigned long long *>(uni_scratch);
-    uint32_t *log_n = reinterpret_cast<uint32_t *>(uni + ntables);
-    TsLog *logs = reinterpret_cast<TsLog *>(reinterpret_cast<uint8_t *>(log_n) + (((size_t)ntables * 4 + 255) & ~(size_t)255));
+    uint8_t *sp = static_cast<uint8_t *>(uni_scratch);
+    unsigned long long *uni = reinterpret_cast<unsigned long long *>(sp);
+    sp += al256((size_t)ntables * 8);
+    uint32_t *log_n = reinterpret_cast<uint32_t *>(sp);
+    sp += al256((size_t)ntables * 4);
+    TsLog *logs = reinterpret_cast<TsLog *>(sp);
+    sp += al256((size_t)ntables * TS_LOG_CAP * sizeof(TsLog));
+    TsSeg *segs = reinterpret_cast<TsSeg *>(sp);
+    sp += al256((size_t)ntables * TS_SEGS * sizeof(TsSeg));
+    TsWin *wins = reinterpret_cast<TsWin *>(sp);
     hipError_t e = hipMemsetAsync(uni, 0xff, tscan_uni_bytes(ntables), L.stream);
     if (e != hipSuccess) return e;
     for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // gridDim.y <= 65535
@@ -365,6 +634,13 @@ hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *tab
         hipLaunchKernelGGL((k_tscan_uni<false>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src, table_off + t0,
                            mode, uni + t0, out, max_out, first + t0);
     }
+    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // segment walks, then the stitch per table
+        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
+        hipLaunchKernelGGL(k_tscan_seg, dim3(TS_SEGS, m), dim3(TS_THREADS), 0, L.stream, src, table_off + t0, mode,
+                           uni + t0, segs + (size_t)t0 * TS_SEGS, wins + (size_t)t0 * TS_SEGS * TS_SEG_LOG);
+    }
+    hipLaunchKernelGGL(k_tscan_stitch, dim3(ntables), dim3(64), 0, L.stream, src, table_off, mode, uni, segs, wins,
+                       first, out_end, log_n);
     hipLaunchKernelGGL((k_tscan<false>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
                        max_out, first, out_end, uni, logs, log_n);
     e = hipGetLastError();
@@ -378,6 +654,9 @@ hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *tab
                            table_off + t0, mode, uni + t0, out, max_out, first + t0);
         hipLaunchKernelGGL(k_tscan_logw, dim3(TL_PARTS, m), dim3(TL_THREADS), 0, L.stream, src, table_off + t0, mode,
                            out, max_out, first + t0, logs + (size_t)t0 * TS_LOG_CAP, log_n + t0);
+        hipLaunchKernelGGL(k_tscan_segw, dim3(TS_SEGS, m), dim3(TS_THREADS), 0, L.stream, src, table_off + t0, mode,
+                           uni + t0, segs + (size_t)t0 * TS_SEGS, wins + (size_t)t0 * TS_SEGS * TS_SEG_LOG, log_n + t0,
+                           first + t0, out, max_out);
     }
     hipLaunchKernelGGL((k_tscan<true>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
                        max_out, first, out_end, uni, logs, log_n);

@@ -121,6 +121,25 @@ def test_uniform_prefix_edges(codec, mode):
     assert check(codec, tables, mode) > 42000
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_segment_walks_and_their_misses(codec, mode):
+    """Tables past 1 MiB are walked as up to 64 segments from guessed entry points and stitched
+    (k_tscan_seg / k_tscan_stitch / k_tscan_segw).  Random values: the guesses hold.  Values
+    that hold 10 record-shaped sub-records and then noise: a segment that starts early in such a
+    value guesses a sub-record chain that survives the guess test but never meets the true chain,
+    so the stitch misses and the table takes the serial walk.  Both must match the restatement,
+    as must a chain that jumps over whole segments (one 3-MiB value)."""
+    rng = random.Random(21)
+    recs = [rec(rand_bytes(rng, rng.randrange(8, 40)), rand_bytes(rng, rng.randrange(100, 4000)), seq=i + 1)
+            for i in range(3000)]
+    plain = b"".join(recs)
+    sub = lambda: b"".join(struct.pack("<III", 2, 3, 1) + b"ab" + b"xyz" for _ in range(10))
+    nested = b"".join(rec(rand_bytes(rng, 16), sub() + rand_bytes(rng, 7), seq=i + 1) for i in range(60000))
+    jump = b"".join(recs[:100]) + rec(b"huge", rand_bytes(rng, 3 << 20)) + b"".join(recs[100:300])
+    tables = [plain + bytes(12), nested + bytes(12), jump + bytes(12), plain * 3]
+    assert check(codec, tables, mode) > 60000
+
+
 def test_step_log_overflow_falls_back_to_the_serial_walk(codec):
     """The write pass replays the count walk's logged steps (k_tscan_logw); a table whose walk
     takes more than TS_LOG_CAP = 4,096 steps (here ~4,300 windows of 128 KiB: a 540-MB table of
