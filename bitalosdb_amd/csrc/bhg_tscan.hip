@@ -314,12 +314,19 @@ __global__ __launch_bounds__(TL_THREADS) void k_tscan_logw(const uint8_t *__rest
 // After the uniform prefix (end P) a table's region [P, tlen) is cut into TS_SEGS segments.
 // k_tscan_seg: segment j's workgroup guesses where the record chain enters it (j = 0: P itself;
 // else the first of its first 64 KiB of positions whose chain survives TS_SURVIVE headers inside
-// the staged 128-KiB window, or ends there in a terminator or exactly at the data's end), walks the chain from there to the first node at or past the segment's end, and logs its
+// the staged window, or ends there in a terminator or exactly at the data's end), walks the chain from there to the first node at or past the segment's end, and logs its
 // windows.  k_tscan_stitch then follows the true chain: where it enters segment j at e, e must
 // be a node of that walk (re-chased from the logged window holding e), and the walk's records
 // from e on are the table's.  A miss (no guess, a wrong guess, a log overflow) sends the table
 // to the serial walk (k_tscan), so a guess never decides a result.
-constexpr uint32_t TS_SEGS = 64, TS_SEG_LOG = 256, TS_PROBE = 64 * 1024, TS_SURVIVE = 8;
+#ifndef BHG_SEG_WIN_KB
+#define BHG_SEG_WIN_KB 64
+#endif
+// segment walks: 512-thread workgroups with 64-KiB windows, two per CU (a CU's two walks hide each
+// other's window loads); guesses probed in the window's first half
+constexpr int SG_THREADS = BHG_SEG_WIN_KB == 128 ? 1024 : 512;
+constexpr uint32_t SG_WIN = BHG_SEG_WIN_KB * 1024u;
+constexpr uint32_t TS_SEGS = 64, TS_SEG_LOG = 256, TS_PROBE = SG_WIN / 2, TS_SURVIVE = 8;
 constexpr uint64_t TS_SEG_MIN = 1ull << 20;
 struct TsSeg {
     uint64_t g, cnt, x;  // guessed entry; records walked in [g, segment end); where the walk stopped
@@ -358,11 +365,11 @@ __device__ __forceinline__ int seg_step(uint64_t off, uint64_t s1, uint64_t tlen
     return 0;
 }
 
-__global__ __launch_bounds__(TS_THREADS) void k_tscan_seg(const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(SG_THREADS) void k_tscan_seg(const uint8_t *__restrict__ src,
                                                           const uint64_t *__restrict__ table_off, int mode,
                                                           const unsigned long long *__restrict__ uni,
                                                           TsSeg *__restrict__ segs, TsWin *__restrict__ wins) {
-    __shared__ alignas(16) uint8_t win[TS_WIN];
+    __shared__ alignas(16) uint8_t win[SG_WIN];
     __shared__ uint32_t s_best, s_nlog;
     __shared__ uint64_t s_off, s_cnt;
     __shared__ int s_state;
@@ -379,17 +386,17 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan_seg(const uint8_t *__restr
         return;
     }
     auto stage = [&](uint64_t wbeg) -> uint64_t {  // [wbeg, we) into LDS; returns we
-        const uint64_t we = tlen - wbeg < TS_WIN ? tlen : wbeg + TS_WIN;
+        const uint64_t we = tlen - wbeg < SG_WIN ? tlen : wbeg + SG_WIN;
         const uint32_t wlen = (uint32_t)(we - wbeg);
-        if (wlen == TS_WIN) {
-            constexpr uint32_t PER = TS_WIN / (TS_THREADS * 16);
+        if (wlen == SG_WIN) {
+            constexpr uint32_t PER = SG_WIN / (SG_THREADS * 16);
             u32x4 r[PER];
 #pragma unroll
-            for (uint32_t q = 0; q < PER; q++) r[q] = gld<u32x4_a4>(t0 + wbeg + 16 * (q * TS_THREADS + tid));
+            for (uint32_t q = 0; q < PER; q++) r[q] = gld<u32x4_a4>(t0 + wbeg + 16 * (q * SG_THREADS + tid));
 #pragma unroll
-            for (uint32_t q = 0; q < PER; q++) *reinterpret_cast<u32x4_a4 *>(win + 16 * (q * TS_THREADS + tid)) = r[q];
+            for (uint32_t q = 0; q < PER; q++) *reinterpret_cast<u32x4_a4 *>(win + 16 * (q * SG_THREADS + tid)) = r[q];
         } else {
-            for (uint32_t b = tid * 16; b < wlen; b += TS_THREADS * 16) {
+            for (uint32_t b = tid * 16; b < wlen; b += SG_THREADS * 16) {
                 if (b + 16 <= wlen) *reinterpret_cast<u32x4_a4 *>(win + b) = gld<u32x4_a4>(t0 + wbeg + b);
                 else for (uint32_t q = b; q < wlen; q++) win[q] = gld<uint8_t>(t0 + wbeg + q);
             }
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan_seg(const uint8_t *__restr
     __syncthreads();
     if (j > 0) {  // the guess: the first probed position whose chain survives TS_SURVIVE headers
         const uint64_t lim = s1 - s0 < TS_PROBE ? s1 - s0 : TS_PROBE;
-        for (uint32_t c = tid; c < lim; c += TS_THREADS) {
+        for (uint32_t c = tid; c < lim; c += SG_THREADS) {
             uint64_t q = s0 + c;
             uint32_t n = 0;
             bool acc = false;
@@ -498,15 +505,19 @@ __global__ __launch_bounds__(64) void k_tscan_stitch(const uint8_t *__restrict__
         TsSeg &sg = segs[(uint64_t)t * TS_SEGS + j];
         if (e >= s1) continue;  // the chain jumped over this segment (r stays ~0: nothing written)
         if (!(sg.flags & TSF_WALKED) || (sg.flags & TSF_FAIL) || e < sg.g) { ok = false; break; }
-        // the logged window holding e: the last one starting at or before e
-        const TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
-        uint32_t lo = 0, hi = sg.nlog;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (wl[mid].off <= e) lo = mid; else hi = mid;
+        uint64_t off = e, c = 0, we = 0;
+        if (e != sg.g) {  // (the guess is the entry: record 0, nothing to check)
+            // the logged window holding e: the last one starting at or before e
+            const TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
+            uint32_t lo = 0, hi = sg.nlog;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (wl[mid].off <= e) lo = mid; else hi = mid;
+            }
+            off = wl[lo].off;
+            c = wl[lo].cnt;
+            we = wl[lo].we;
         }
-        uint64_t off = wl[lo].off, c = wl[lo].cnt;
-        const uint64_t we = wl[lo].we;
         while (off < e) {
             uint64_t adv = 0;
             uint32_t k = 0, v = 0;
@@ -636,7 +647,7 @@ hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *tab
     }
     for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // segment walks, then the stitch per table
         const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
-        hipLaunchKernelGGL(k_tscan_seg, dim3(TS_SEGS, m), dim3(TS_THREADS), 0, L.stream, src, table_off + t0, mode,
+        hipLaunchKernelGGL(k_tscan_seg, dim3(TS_SEGS, m), dim3(SG_THREADS), 0, L.stream, src, table_off + t0, mode,
                            uni + t0, segs + (size_t)t0 * TS_SEGS, wins + (size_t)t0 * TS_SEGS * TS_SEG_LOG);
     }
     hipLaunchKernelGGL(k_tscan_stitch, dim3(ntables), dim3(64), 0, L.stream, src, table_off, mode, uni, segs, wins,
