@@ -326,7 +326,8 @@ __global__ __launch_bounds__(TL_THREADS) void k_tscan_logw(const uint8_t *__rest
 // other's window loads); guesses probed in the window's first half
 constexpr int SG_THREADS = BHG_SEG_WIN_KB == 128 ? 1024 : 512;
 constexpr uint32_t SG_WIN = BHG_SEG_WIN_KB * 1024u;
-constexpr uint32_t TS_SEGS = 64, TS_SEG_LOG = 256, TS_PROBE = SG_WIN / 2, TS_SURVIVE = 8;
+constexpr uint32_t TS_SEGS = 64, TS_SEG_LOG = 512, TS_PROBE = SG_WIN / 2, TS_SURVIVE = 8;
+constexpr uint32_t TS_SEG_GROUP = 32;  // a log entry every 32 records too: the replay's unit of work
 constexpr uint64_t TS_SEG_MIN = 1ull << 20;
 struct TsSeg {
     uint64_t g, cnt, x;  // guessed entry; records walked in [g, segment end); where the walk stopped
@@ -462,6 +463,10 @@ __global__ __launch_bounds__(SG_THREADS) void k_tscan_seg(const uint8_t *__restr
                 if (r != 0) { state = r; break; }
                 cnt++;
                 off += adv;
+                if (cnt % TS_SEG_GROUP == 0) {
+                    if (nlog < TS_SEG_LOG) wl[nlog] = TsWin{off, cnt, we};
+                    nlog++;
+                }
             }
             s_off = off;
             s_cnt = cnt;
@@ -542,7 +547,8 @@ __global__ __launch_bounds__(64) void k_tscan_stitch(const uint8_t *__restrict__
     }
 }
 
-// the write pass of the segment walks: one wave per logged window, records from the stitch's r on
+// the write pass of the segment walks: one lane per logged entry (a window start or every 32nd
+// record), records from the stitch's r on
 __global__ __launch_bounds__(TS_THREADS) void k_tscan_segw(const uint8_t *__restrict__ src,
                                                            const uint64_t *__restrict__ table_off, int mode,
                                                            const unsigned long long *__restrict__ uni,
@@ -562,11 +568,11 @@ __global__ __launch_bounds__(TS_THREADS) void k_tscan_segw(const uint8_t *__rest
     const TsWin *wl = wins + ((uint64_t)t * TS_SEGS + j) * TS_SEG_LOG;
     const uint64_t w0 = first[t] + sg.base;
     const uint32_t nl = sg.nlog;
-    for (uint32_t q = wv; q < nl; q += TS_WAVES) {
-        if (lane != 0) continue;
+    for (uint32_t q = wv * 64 + lane; q < nl; q += TS_THREADS) {  // a lane per logged entry
         const TsWin w = wl[q];
+        const uint64_t cend = q + 1 < nl ? wl[q + 1].cnt : sg.cnt;  // the entry's records: [w.cnt, cend)
         uint64_t off = w.off, c = w.cnt;
-        for (;;) {
+        while (c < cend) {
             uint32_t k = 0, v = 0;
             if (off + 12 <= tlen) { k = ldu32(t0 + off, tend); v = ldu32(t0 + off + 4, tend); }
             uint64_t adv = 0;
