@@ -3,8 +3,12 @@
 // Writer.rebuild (bithash/writer.go:539-583, mode 1).
 //
 // A record's start depends on the previous header, so each
-// table is one dependency chain; one 1024-thread workgroup walks it.
-// Two moves alternate:
+// table is one dependency chain.  Stages: the uniform prefix of every table,
+// grid-wide (k_tscan_uni); speculative segment walks from guessed entries and
+// their stitch (k_tscan_seg / k_tscan_stitch, below), which resolve a table
+// whenever the true chain meets every segment walk it enters; for any other
+// table, the serial walk of one 1024-thread workgroup (k_tscan), in which two
+// moves alternate:
 //  * speculation (uniform record lengths -- the common bulk-load case):
 //    from a known start `off` with the last record length G, thread i reads
 //    the header at off + i*G.  Threads up to the first one whose length is
