@@ -317,8 +317,8 @@ __global__ __launch_bounds__(TL_THREADS) void k_tscan_logw(const uint8_t *__rest
 // ---- speculative segment walks (mixed lengths) ----
 // After the uniform prefix (end P) a table's region [P, tlen) is cut into TS_SEGS segments.
 // k_tscan_seg: segment j's workgroup guesses where the record chain enters it (j = 0: P itself;
-// else the first of its first 64 KiB of positions whose chain survives TS_SURVIVE headers inside
-// the staged window, or ends there in a terminator or exactly at the data's end), walks the chain from there to the first node at or past the segment's end, and logs its
+// else the first of its first 32 KiB of positions whose chain survives TS_SURVIVE headers, or 3
+// before it leaves the staged window, or ends in a terminator or exactly at the data's end), walks the chain from there to the first node at or past the segment's end, and logs its
 // windows.  k_tscan_stitch then follows the true chain: where it enters segment j at e, e must
 // be a node of that walk (re-chased from the logged window holding e), and the walk's records
 // from e on are the table's.  A miss (no guess, a wrong guess, a log overflow) sends the table
@@ -428,10 +428,11 @@ __global__ __launch_bounds__(SG_THREADS) void k_tscan_seg(const uint8_t *__restr
                 if (q > tlen) break;
                 const uint64_t rem = tlen - q;
                 if (rem < 12) { acc = n > 0; break; }
-                // a chain that leaves the staged window is not taken: false headers jump anywhere
-                // up to 4 GB, and one landing on a true record later merges with the true chain
-                // (measured: 3 of 16 scanmix tables missed); 8 true records of <= 4 KiB stay inside
-                if (q + 8 > we) break;
+                // a chain that leaves the staged window counts only after 3 records inside it:
+                // false headers jump anywhere up to 4 GB, and one landing on a true record later
+                // merges with the true chain (taking any chain that left: 3 of 16 scanmix tables
+                // missed); three in-window steps of a false chain are ~1e-14 likely
+                if (q + 8 > we) { acc = n >= 3; break; }
                 uint32_t k, v;
                 hdr_lds(q, wb, k, v);
                 const Hdr hh = hdr_rule(rem, k, v, mode);

@@ -136,7 +136,9 @@ def test_segment_walks_and_their_misses(codec, mode):
     sub = lambda: b"".join(struct.pack("<III", 2, 3, 1) + b"ab" + b"xyz" for _ in range(10))
     nested = b"".join(rec(rand_bytes(rng, 16), sub() + rand_bytes(rng, 7), seq=i + 1) for i in range(60000))
     jump = b"".join(recs[:100]) + rec(b"huge", rand_bytes(rng, 3 << 20)) + b"".join(recs[100:300])
-    tables = [plain + bytes(12), nested + bytes(12), jump + bytes(12), plain * 3]
+    large = b"".join(rec(rand_bytes(rng, 24), rand_bytes(rng, rng.randrange(5000, 12000)), seq=i + 1)
+                     for i in range(1500))  # a guess may leave the window after 3 records
+    tables = [plain + bytes(12), nested + bytes(12), jump + bytes(12), plain * 3, large + bytes(12)]
     assert check(codec, tables, mode) > 60000
 
 
