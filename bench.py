@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     # GPU clocks ramp over the first ~100 C2 launches (~30 ms of load; profiles/r1_s6_clock_ramp_probe.txt)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--ramp-ms", type=float, default=300.0,
+                    help="untimed steps of the measured kernel for at least this long before the --warmup steps "
+                         "(the MI355X clocks ramp over tens of ms of load); 0 disables; recorded in the line")
     ap.add_argument("--blocks", type=int, default=1_000_000, help="blocks per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -417,10 +420,10 @@ def c2_measure(a, world, rank, local, dev, codec, with_extras):
     def step():
         codec.decode_batch(src_t, src_t.numel(), h_t, n, expected_crc=exp_crc, out_desc=desc_t)
 
-    # the measured D2D copy ceiling of the same bytes, taken BEFORE the warm-up steps: its ~40 ms of
-    # HBM streaming also brings the MI355X clocks out of idle (they ramp over ~30 ms of load,
-    # profiles/r1_s6_clock_ramp_probe.txt), so a short --warmup times steady-state clocks
+    # the measured D2D copy ceiling of the same bytes (before the warm-up steps), then the stated
+    # clock ramp (clock_ramp: --ramp-ms of untimed steps), then the --warmup steps
     copy_gbps, copy_ms = copy_ceiling(src_t, dev, reps=100)
+    ramp = clock_ramp(a, dev, step)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -476,6 +479,7 @@ def c2_measure(a, world, rank, local, dev, codec, with_extras):
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "ramp": ramp,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -492,8 +496,8 @@ def c2_measure(a, world, rank, local, dev, codec, with_extras):
                      "algorithmic_bytes_per_block": ALGO_BYTES_PER_BLOCK + 4,
                      "measured_copy_ceiling": {"GBps": round(copy_gbps, 1), "ms": round(copy_ms, 4),
                                                "what": "torch D2D copy of the same %d B (read + write), "
-                                                       "100 reps run before the warm-up steps (they also ramp "
-                                                       "the clocks)" % src_t.numel(),
+                                                       "100 reps run before the clock ramp and the warm-up "
+                                                       "steps" % src_t.numel(),
                                                "frac_of_copy": round(achieved / copy_gbps, 4)}},
         "status_ok_blocks": int(ok_total),
         "valid": bool(ok_total == n_total),
@@ -677,7 +681,27 @@ def _encode_tables(codec, n, val_lens, dev, seed, compressor, gen="dict"):
     return out[:total], h, dict(src_bytes=total, ntables=int(bufs.summary[1].item())), (keys, key_off, tr, vals, val_off, bufs)
 
 
+def clock_ramp(a, dev, fn):
+    """Untimed steps of the measured path for >= a.ramp_ms of wall time, before the --warmup steps:
+    the clocks come out of idle over tens of ms of load, so without it a short --warmup (the driver
+    runs --warmup 5) times part of the ramp.  Returns the record put in the JSON line."""
+    if a.ramp_ms <= 0:
+        return {"ms": 0.0, "steps": 0}
+    torch.cuda.synchronize(dev)
+    t0, k = time.perf_counter(), 0
+    while True:
+        for _ in range(8):
+            fn()
+        k += 8
+        torch.cuda.synchronize(dev)
+        if (time.perf_counter() - t0) * 1e3 >= a.ramp_ms:
+            break
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": k,
+            "what": "untimed steps of the measured kernel before the --warmup steps (clock ramp)"}
+
+
 def _timed(a, dev, fn):
+    a.ramp_record = clock_ramp(a, dev, fn)
     for _ in range(a.warmup):
         fn()
     torch.cuda.synchronize(dev)
@@ -731,7 +755,8 @@ def c3_measure(a, world, rank, local, dev, codec, gen, extras):
     disk = float(h["length"].astype(np.float64).sum())
     out = {"metric": "GiB/s bithash blocks decoded (device-resident), snappy, 32B key / 1KB value, 1 GPU",
            "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "warmup": a.warmup, "ramp": a.ramp_record, "ms_per_step": round(el / a.steps * 1e3, 4),
+           "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (GPU-encoded snappy tables, values: %s)" % gen,
            "config": {"workload": "BASELINE configs[2]: 1M snappy blocks, CRC-verify (expected_crc = the writer's "
@@ -862,7 +887,8 @@ def c4_measure(a, world, rank, local, dev, codec, gen, extras):
     total = int(bufs.summary[0].item())
     res = {"metric": "GiB/s KV input encoded (record-pack + snappy + CRC), values 64B-4KB, 1 GPU",
            "value": round(raw * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "warmup": a.warmup, "ramp": a.ramp_record, "ms_per_step": round(el / a.steps * 1e3, 4),
+           "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic compressible values (%s)" % gen,
            "config": {"workload": "BASELINE configs[3]: 1M KV pairs -> record-pack + compress + CRC",
@@ -966,7 +992,8 @@ def mixdec_measure(a, world, rank, local, dev, codec, compressor, extras):
     name = "snappy" if compressor else "NoCompressor"
     out = {"metric": "GiB/s bithash blocks decoded (device-resident), %s, C4 value mix 64B-4KB, 1 GPU" % name,
            "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "warmup": a.warmup, "ramp": a.ramp_record, "ms_per_step": round(el / a.steps * 1e3, 4),
+           "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (GPU-encoded %s tables, values: %s)" % (name, a.values),
            "config": {"workload": "decode of the C4-shaped tables: 1M pairs, 32 B keys, values U[64, 4096] B, "
@@ -1047,6 +1074,7 @@ def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
             codec.decode_batch(src_t, src_t.numel(), h_t, n, 1 if snappy else 0, expected_crc=exp_crc,
                                out_desc=desc_t, out_vals=vals_t, out_val_off=voff_t)
 
+    ramp = clock_ramp(a, dev, step)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -1088,6 +1116,7 @@ def c5_measure(a, world, rank, local, dev, codec, codec_name, with_cpu):
         "metric": "GiB/s bithash table files decoded (device-resident), 25 GB corpus sharded by table, "
                   "32B key / 1KB value",
         "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ramp": ramp,
         "ms_per_step": round(el_max / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (per-table seeded generator: a table's bytes do not depend on N)",
@@ -1170,7 +1199,8 @@ def run_scan(a, world, rank, local, dev, codec):
     scanned = float(toff[-1])
     res = {"metric": "GiB/s table data regions scanned (TableIterator header chase), 1 GPU",
            "value": round(scanned * a.steps / el / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+           "warmup": a.warmup, "ramp": a.ramp_record, "ms_per_step": round(el / a.steps * 1e3, 4),
+           "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
            "config": {"workload": "row A4 table scan: " + what, "records_per_gpu": n, "tables": ntab,
                       "bytes": int(scanned), "Mrecords_per_s": round(n * a.steps / el / 1e6, 2)},

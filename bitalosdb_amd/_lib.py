@@ -25,7 +25,8 @@ CODEC_NONE, CODEC_SNAPPY = 0, 1
 ST_OK, ST_RECORD_NIL, ST_ILLEGAL_LENGTH, ST_INCOMPLETE, ST_SNAPPY_CORRUPT, ST_SNAPPY_TOO_LARGE, \
     ST_CRC_MISMATCH, ST_KEY_TOO_LARGE, ST_VALUE_TOO_LARGE, ST_DATA_MAX_EXCEEDED, ST_NOT_FOUND, \
     ST_NO_SPACE, ST_SKIPPED, ST_FILE_NUM_ZERO = range(14)
-ABI_VERSION = 2
+SCAN_PATH_SEGMENTS, SCAN_PATH_REPLAY, SCAN_PATH_SERIAL = range(3)
+ABI_VERSION = 3
 TABLE_DT = np.dtype([("base", "<u8"), ("index_off", "<u8"), ("index_len", "<u8"), ("conflict_off", "<u8"),
                      ("conflict_bh_off", "<u4"), ("conflict_bh_len", "<u4")])
 WRITER_INDEX_DT = np.dtype([("rec", "<u8"), ("sorted", "<u8"), ("sorted_kh", "<u8"), ("n", "<u4"),
@@ -40,7 +41,7 @@ EXPORTS = [
     "bhg_encode_ikey_batch", "bhg_scan_tables", "bhg_table_tail", "bhg_rebuild_tables",
     "bhg_repack_batch",
     "bhg_host_register", "bhg_host_unregister", "bhg_get_batch", "bhg_writer_index_build",
-    "bhg_bithash_get_batch",
+    "bhg_bithash_get_batch", "bhg_scan_tables_paths", "bhg_scan_scratch_bytes",
 ]
 
 
@@ -98,6 +99,8 @@ def lib():
             "bhg_encode_ikey_batch": (I, [P, P, P, P, P, P, U32, P, P, P, U32, P, U64,
                                           ctypes.POINTER(EncodeOut), P]),
             "bhg_scan_tables": (I, [P, P, P, U32, I, P, U64, P, P, P]),
+            "bhg_scan_tables_paths": (I, [P, P, P, U32, I, P, U64, P, P, P, P]),
+            "bhg_scan_scratch_bytes": (U64, [U32]),
             "bhg_table_tail": (I, [P, P, P, P, P, P, P, U32, U32, P, P, U64, P, P, P, P]),
             "bhg_rebuild_tables": (I, [P, P, P, U32, P, U64, P, P, P, P, P, P]),
             "bhg_repack_batch": (I, [P, P, U64, P, U32, P, P, U32, P, U64, ctypes.POINTER(EncodeOut), P]),

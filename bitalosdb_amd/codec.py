@@ -407,18 +407,20 @@ class BithashCodec:
         B.check(self.ctx, rc, "bhg_rebuild_tables")
         return h[:cnt], first, end[:ntab], kh[:cnt], bo[:cnt], tb[:cnt]
 
-    def scan_tables(self, src_t, table_off, mode=0, max_out=None):
+    def scan_tables(self, src_t, table_off, mode=0, max_out=None, paths=False):
         """TableIterator (mode 0, table.go:358-395) / Writer.rebuild (mode 1,
         writer.go:539-583) header chase over each table src_t[table_off[t]:table_off[t+1]].
 
         Returns device tensors (handles [count] HANDLE_DT-shaped int64 pairs,
         first [ntables+1] int64, end [ntables] int64).  max_out=None counts first
-        (one extra scan) and sizes the handle buffer exactly."""
+        (one extra scan) and sizes the handle buffer exactly.  paths=True adds a
+        fourth tensor: per table, the pass that wrote its handles (B.SCAN_PATH_*)."""
         ntab = len(table_off) - 1
         with torch.cuda.stream(self.stream):
             toff = table_off if torch.is_tensor(table_off) else _u64_tensor(table_off, self.device)
             first = torch.zeros(ntab + 1, dtype=torch.int64, device=self.device)
             end = torch.zeros(max(ntab, 1), dtype=torch.int64, device=self.device)
+            path = torch.full((max(ntab, 1),), -1, dtype=torch.int32, device=self.device)
         if max_out is None:
             rc = self.L.bhg_scan_tables(self.ctx, _ptr(src_t), _ptr(toff), ntab, mode, None, 0, _ptr(first),
                                         _ptr(end), self._stream())
@@ -427,6 +429,11 @@ class BithashCodec:
             max_out = int(first[ntab].item())
         with torch.cuda.stream(self.stream):
             out = torch.empty((max(max_out, 1), 2), dtype=torch.int64, device=self.device)
+        if paths:
+            rc = self.L.bhg_scan_tables_paths(self.ctx, _ptr(src_t), _ptr(toff), ntab, mode, _ptr(out), max_out,
+                                              _ptr(first), _ptr(end), _ptr(path), self._stream())
+            B.check(self.ctx, rc, "bhg_scan_tables_paths")
+            return out[:max_out], first, end[:ntab], path[:ntab]
         rc = self.L.bhg_scan_tables(self.ctx, _ptr(src_t), _ptr(toff), ntab, mode, _ptr(out), max_out, _ptr(first),
                                     _ptr(end), self._stream())
         B.check(self.ctx, rc, "bhg_scan_tables")

@@ -272,6 +272,15 @@ bhg_ctx *bhg_create(int device, int flags) {
         ok = hipMalloc(reinterpret_cast<void **>(&c->xtab), z.size() * 4) == hipSuccess &&
              hipMemcpy(c->xtab, z.data(), z.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
+    if (ok) {  // the LDS store ordering the snappy encoder relies on (bhg_snappy_enc.hip k_lds_order_probe)
+        uint32_t *bad = nullptr, h = 1;
+        ok = hipMalloc(reinterpret_cast<void **>(&bad), 4) == hipSuccess &&
+             bhg::launch_lds_order_probe(c->stream, bad) == hipSuccess &&
+             hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+             hipStreamSynchronize(c->stream) == hipSuccess && h == 0;
+        if (bad) (void)hipFree(bad);
+        if (!ok) fprintf(stderr, "bithashgpu: device %d failed the LDS store-ordering probe\n", device);
+    }
     if (!ok) {
         bhg_destroy(c);
         return nullptr;
@@ -1132,8 +1141,10 @@ int bhg_repack_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     return BHG_OK;
 }
 
-int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
-                    bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end, void *stream) {
+namespace {
+int scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end, uint32_t *out_path,
+                void *stream) {
     if (!c) return BHG_EINVAL;
     if (mode != 0 && mode != 1) { set_err(c, "bad scan mode %d", mode); return BHG_EINVAL; }
     if (!out_first) { set_err(c, "scan needs out_first[ntables+1]"); return BHG_EINVAL; }
@@ -1145,8 +1156,25 @@ int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, u
     const size_t sb = (bhg::scan_scratch_bytes(ntables) + 255) & ~(size_t)255;
     if (int r = scratch_alloc(c, L.stream, sb + bhg::tscan_uni_bytes(ntables), sc)) return r;
     HIP_TRY(c, bhg::launch_tscan(L, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, sc.base,
-                                 static_cast<uint8_t *>(sc.base) + sb));
+                                 static_cast<uint8_t *>(sc.base) + sb, out_path));
     return BHG_OK;
+}
+}  // namespace
+
+int bhg_scan_tables(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                    bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end, void *stream) {
+    return scan_tables(c, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, nullptr, stream);
+}
+
+int bhg_scan_tables_paths(bhg_ctx *c, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                          bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
+                          uint32_t *out_path, void *stream) {
+    if (!out_path && ntables) { set_err(c, "null out_path"); return BHG_EINVAL; }
+    return scan_tables(c, src, table_off, ntables, mode, out_handles, max_out, out_first, out_end, out_path, stream);
+}
+
+uint64_t bhg_scan_scratch_bytes(uint32_t ntables) {
+    return ((bhg::scan_scratch_bytes(ntables) + 255) & ~(size_t)255) + bhg::tscan_uni_bytes(ntables);
 }
 
 int bhg_table_tail(bhg_ctx *c, const uint8_t *recs, const bhg_handle *rec, const uint32_t *bh_off,

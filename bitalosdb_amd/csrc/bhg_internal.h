@@ -188,8 +188,11 @@ hipError_t launch_copy_out(const Launch &L, const uint8_t *src, uint8_t *dst, ui
 // bhg_tscan.hip: table data-region scan (uniform prefixes -> count -> scan -> write); first[ntables+1],
 // scan_scratch holds scan_scratch_bytes(ntables), uni_scratch tscan_uni_bytes(ntables).
 size_t tscan_uni_bytes(uint32_t ntables);
+// bhg_snappy_enc.hip: *bad = 0 iff the highest lane's byte stays when lanes of one ds_write_b8
+// store to the same byte (the encoder's duplicate-bucket check relies on it)
+hipError_t launch_lds_order_probe(hipStream_t stream, uint32_t *bad);
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                         bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
-                        void *uni_scratch);
+                        void *uni_scratch, uint32_t *out_path = nullptr);
 
 }  // namespace bhg

@@ -235,6 +235,39 @@ __device__ uint64_t se_prof[8];  // lab: cycles in scan / copy loop / flushes, c
 #define SE_T(x)
 #endif
 
+// The one LDS property se_batch's duplicate-bucket check relies on: when several lanes of ONE
+// ds_write_b8 store to the same byte, the highest lane's byte is the one that stays.  This code
+// cites no ISA rule for it, so bhg_create runs this probe on every device and refuses a device
+// where it fails: the encoder never runs on an unchecked ordering.  64 mappings of the
+// 64 lanes onto 1 .. 64 bytes; *bad counts the bytes that kept another lane's value.
+__global__ __launch_bounds__(64) void k_lds_order_probe(uint32_t *bad) {
+    __shared__ uint32_t words[64];
+    uint8_t *const db = reinterpret_cast<uint8_t *>(words);
+    const uint32_t lane = threadIdx.x;
+    uint32_t errs = 0;
+    for (uint32_t pat = 0; pat < 64; pat++) {
+        const uint32_t nb = 1u << (pat % 7);  // 1 .. 64 distinct bytes
+        const uint32_t idx = (((lane + 7 * pat) * 0x9E3779B1u) >> 20) % nb + 64 * (pat & 1);
+        words[lane] = 0;
+        wsync();
+        db[idx] = (uint8_t)(lane + 1);
+        wsync();
+        const uint32_t got = db[idx];
+        wsync();
+        uint32_t hi = 0;
+        for (uint32_t j = 0; j < 64; j++)
+            if ((uint32_t)__builtin_amdgcn_readlane((int)idx, (int)j) == idx) hi = j;
+        errs += got != hi + 1;
+    }
+    errs = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__popcll(__ballot(errs != 0)));
+    if (lane == 0) *bad = errs;
+}
+
+hipError_t launch_lds_order_probe(hipStream_t stream, uint32_t *bad) {
+    hipLaunchKernelGGL(k_lds_order_probe, dim3(1), dim3(64), 0, stream, bad);
+    return hipGetLastError();
+}
+
 // The end of one scan batch (lane = one iteration of encodeBlock's candidate loop, in order;
 // lanes >= nl are not part of it): candidates read from the table as it was before the batch
 // are corrected for buckets that two lanes share (the latest earlier lane wins -- Go stores
@@ -249,7 +282,8 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
     // lanes whose bucket (h mod 1024) a HIGHER lane of the batch shares: every lane writes its
     // lane number + 1 into the bucket's byte and reads it back -- in one LDS store instruction the
-    // highest lane's byte is the one that stays, so exactly the lanes below another lane of their
+    // highest lane's byte is the one that stays (checked on the device by k_lds_order_probe when
+    // the context is created), so exactly the lanes below another lane of their
     // bucket read a foreign byte (the highest lane of a bucket has no lane above it to hand its
     // position to, and nothing to learn from the walk: its nxt stays 64).  Invalid lanes write
     // into their own scratch bytes.  Two LDS operations, no atomics (the per-bucket counters

@@ -631,57 +631,85 @@ hipError_t launch_rebuild_recs(const Launch &L, const uint8_t *src, const uint64
 }
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// The walk's scratch (uniform prefixes, step logs, segment walks and their window logs) is ~0.9 MiB
+// per table; tables are scanned TS_CHUNK at a time through one scratch area, so a call over any
+// number of tables needs at most TS_CHUNK tables' worth (~230 MiB), and only the 12 B per table
+// that are read before they are written (uni, log_n) are filled.
+constexpr uint32_t TS_CHUNK = 256;
+
+// first[0..m] holds a chunk's exclusive scan (first[m] = the chunk's total): add the record
+// count of the tables before the chunk (*carry) and advance *carry past the chunk.
+__global__ __launch_bounds__(256) void k_tscan_carry(uint64_t *first, uint32_t m, uint64_t *carry, int first_chunk) {
+    const uint64_t c = first_chunk ? 0ull : *carry;
+    const uint64_t tot = first[m];
+    __syncthreads();  // every read above happens before first[m] or *carry is rewritten
+    for (uint32_t i = threadIdx.x; i <= m; i += blockDim.x) first[i] += c;
+    if (threadIdx.x == 0) *carry = c + tot;
+}
+
+// per table: which pass wrote its handles (BHG_SCAN_PATH_*: segment walks, log replay, serial walk)
+__global__ __launch_bounds__(256) void k_tscan_path(const uint32_t *log_n, uint32_t m, uint32_t *path) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
+        path[i] = log_n[i] == ~0u ? 0u : (log_n[i] <= TS_LOG_CAP ? 1u : 2u);
+}
+
 size_t tscan_uni_bytes(uint32_t ntables) {
-    return al256((size_t)ntables * 8) + al256((size_t)ntables * 4) + al256((size_t)ntables * TS_LOG_CAP * sizeof(TsLog)) +
-           al256((size_t)ntables * TS_SEGS * sizeof(TsSeg)) + (size_t)ntables * TS_SEGS * TS_SEG_LOG * sizeof(TsWin);
+    const size_t m = ntables < TS_CHUNK ? ntables : TS_CHUNK;
+    return 256 + al256(m * 8) + al256(m * 4) + al256(m * TS_LOG_CAP * sizeof(TsLog)) +
+           al256(m * TS_SEGS * sizeof(TsSeg)) + m * TS_SEGS * TS_SEG_LOG * sizeof(TsWin);
 }
 
 hipError_t launch_tscan(const Launch &L, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                         bhg_handle *out, uint64_t max_out, uint64_t *first, uint64_t *out_end, void *scan_scratch,
-                        void *uni_scratch) {
+                        void *uni_scratch, uint32_t *out_path) {
+    const uint32_t M = ntables < TS_CHUNK ? ntables : TS_CHUNK;
     uint8_t *sp = static_cast<uint8_t *>(uni_scratch);
+    uint64_t *carry = reinterpret_cast<uint64_t *>(sp);
+    sp += 256;
     unsigned long long *uni = reinterpret_cast<unsigned long long *>(sp);
-    sp += al256((size_t)ntables * 8);
+    sp += al256((size_t)M * 8);
     uint32_t *log_n = reinterpret_cast<uint32_t *>(sp);
-    sp += al256((size_t)ntables * 4);
+    sp += al256((size_t)M * 4);
     TsLog *logs = reinterpret_cast<TsLog *>(sp);
-    sp += al256((size_t)ntables * TS_LOG_CAP * sizeof(TsLog));
+    sp += al256((size_t)M * TS_LOG_CAP * sizeof(TsLog));
     TsSeg *segs = reinterpret_cast<TsSeg *>(sp);
-    sp += al256((size_t)ntables * TS_SEGS * sizeof(TsSeg));
+    sp += al256((size_t)M * TS_SEGS * sizeof(TsSeg));
     TsWin *wins = reinterpret_cast<TsWin *>(sp);
-    hipError_t e = hipMemsetAsync(uni, 0xff, tscan_uni_bytes(ntables), L.stream);
-    if (e != hipSuccess) return e;
-    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // gridDim.y <= 65535
-        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
-        hipLaunchKernelGGL((k_tscan_uni<false>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src, table_off + t0,
-                           mode, uni + t0, out, max_out, first + t0);
+    hipError_t e = hipSuccess;
+    for (uint32_t c0 = 0; c0 < ntables; c0 += M) {
+        const uint32_t m = ntables - c0 < M ? ntables - c0 : M;
+        const uint64_t *toff = table_off + c0;
+        uint64_t *fst = first + c0;
+        uint64_t *oend = out_end ? out_end + c0 : nullptr;
+        // uni starts at ~0 (atomic min); log_n is written by the stitch for every table, filled anyway.
+        // Segments, logs and windows are written before they are read.
+        if ((e = hipMemsetAsync(uni, 0xff, al256((size_t)M * 8) + (size_t)m * 4, L.stream)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_tscan_uni<false>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src, toff, mode, uni,
+                           out, max_out, fst);
+        // segment walks, then the stitch per table
+        hipLaunchKernelGGL(k_tscan_seg, dim3(TS_SEGS, m), dim3(SG_THREADS), 0, L.stream, src, toff, mode, uni, segs, wins);
+        hipLaunchKernelGGL(k_tscan_stitch, dim3(m), dim3(64), 0, L.stream, src, toff, mode, uni, segs, wins, fst, oend,
+                           log_n);
+        hipLaunchKernelGGL((k_tscan<false>), dim3(m), dim3(TS_THREADS), 0, L.stream, src, toff, mode, out, max_out, fst,
+                           oend, uni, logs, log_n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = launch_exclusive_scan_u64(L, fst, fst, m, scan_scratch)) != hipSuccess) return e;
+        if (ntables > M)
+            hipLaunchKernelGGL(k_tscan_carry, dim3(1), dim3(256), 0, L.stream, fst, m, carry, c0 == 0 ? 1 : 0);
+        if (out_path)
+            hipLaunchKernelGGL(k_tscan_path, dim3((m + 255) / 256), dim3(256), 0, L.stream, log_n, m, out_path + c0);
+        if (out == nullptr || max_out == 0) continue;  // counts and ends only
+        hipLaunchKernelGGL((k_tscan_uni<true>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src, toff, mode, uni,
+                           out, max_out, fst);
+        hipLaunchKernelGGL(k_tscan_logw, dim3(TL_PARTS, m), dim3(TL_THREADS), 0, L.stream, src, toff, mode, out, max_out,
+                           fst, logs, log_n);
+        hipLaunchKernelGGL(k_tscan_segw, dim3(TS_SEGS, m), dim3(TS_THREADS), 0, L.stream, src, toff, mode, uni, segs,
+                           wins, log_n, fst, out, max_out);
+        hipLaunchKernelGGL((k_tscan<true>), dim3(m), dim3(TS_THREADS), 0, L.stream, src, toff, mode, out, max_out, fst,
+                           oend, uni, logs, log_n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {  // segment walks, then the stitch per table
-        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
-        hipLaunchKernelGGL(k_tscan_seg, dim3(TS_SEGS, m), dim3(SG_THREADS), 0, L.stream, src, table_off + t0, mode,
-                           uni + t0, segs + (size_t)t0 * TS_SEGS, wins + (size_t)t0 * TS_SEGS * TS_SEG_LOG);
-    }
-    hipLaunchKernelGGL(k_tscan_stitch, dim3(ntables), dim3(64), 0, L.stream, src, table_off, mode, uni, segs, wins,
-                       first, out_end, log_n);
-    hipLaunchKernelGGL((k_tscan<false>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end, uni, logs, log_n);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    e = launch_exclusive_scan_u64(L, first, first, ntables, scan_scratch);
-    if (e != hipSuccess) return e;
-    if (out == nullptr || max_out == 0) return hipGetLastError();  // counts and ends only
-    for (uint32_t t0 = 0; t0 < ntables; t0 += 65535u) {
-        const uint32_t m = ntables - t0 < 65535u ? ntables - t0 : 65535u;
-        hipLaunchKernelGGL((k_tscan_uni<true>), dim3(TU_PARTS, m), dim3(TU_THREADS), 0, L.stream, src,
-                           table_off + t0, mode, uni + t0, out, max_out, first + t0);
-        hipLaunchKernelGGL(k_tscan_logw, dim3(TL_PARTS, m), dim3(TL_THREADS), 0, L.stream, src, table_off + t0, mode,
-                           out, max_out, first + t0, logs + (size_t)t0 * TS_LOG_CAP, log_n + t0);
-        hipLaunchKernelGGL(k_tscan_segw, dim3(TS_SEGS, m), dim3(TS_THREADS), 0, L.stream, src, table_off + t0, mode,
-                           uni + t0, segs + (size_t)t0 * TS_SEGS, wins + (size_t)t0 * TS_SEGS * TS_SEG_LOG, log_n + t0,
-                           first + t0, out, max_out);
-    }
-    hipLaunchKernelGGL((k_tscan<true>), dim3(ntables), dim3(TS_THREADS), 0, L.stream, src, table_off, mode, out,
-                       max_out, first, out_end, uni, logs, log_n);
     return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BHG_ABI_VERSION 2
+#define BHG_ABI_VERSION 3  /* 3: bhg_bithash_get_batch gained its codec argument (round 5) */
 
 /* ---- API return codes ---- */
 #define BHG_OK 0
@@ -340,6 +340,18 @@ int bhg_rebuild_tables(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_o
 int bhg_scan_tables(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
                     bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
                     void *stream);
+
+/* bhg_scan_tables plus, per table, which pass produced its handles (a diagnostic for tests and
+ * tuning; the handles are the same): out_path[ntables] (device) = BHG_SCAN_PATH_*. */
+#define BHG_SCAN_PATH_SEGMENTS 0  /* segment walks resolved by the stitch */
+#define BHG_SCAN_PATH_REPLAY 1    /* serial count walk, write pass replayed from its step log */
+#define BHG_SCAN_PATH_SERIAL 2    /* serial walk whose step log overflowed: walked again to write */
+int bhg_scan_tables_paths(bhg_ctx *ctx, const uint8_t *src, const uint64_t *table_off, uint32_t ntables, int mode,
+                          bhg_handle *out_handles, uint64_t max_out, uint64_t *out_first, uint64_t *out_end,
+                          uint32_t *out_path, void *stream);
+/* Device scratch (from the context's stream-ordered pool) one scan call over ntables takes: tables
+ * are scanned 256 at a time through one scratch area, so this stops growing at 256 tables. */
+uint64_t bhg_scan_scratch_bytes(uint32_t ntables);
 
 /* ---- batched point lookup (device): Reader.Get minus the pread ----
  * One opened table (NewReader, bithash/reader.go:73-183, done by the host):

@@ -20,7 +20,7 @@ def test_library_builds_and_loads():
     B.build()
     assert os.path.exists(B.LIB_PATH)
     L = B.lib()
-    assert L.bhg_abi_version() == B.ABI_VERSION == 2
+    assert L.bhg_abi_version() == B.ABI_VERSION == 3
 
 
 def test_exports_match_header():
@@ -46,6 +46,16 @@ def test_struct_layouts():
     assert B.DESC_DT.itemsize == 40
     assert B.DESC_DT.fields["trailer"][1] == 16
     assert B.DESC_DT.fields["status"][1] == 36
+
+
+def test_scan_scratch_is_bounded():
+    """the table scan's scratch was ~0.9 MiB per table with no cap.  Tables are now
+    scanned 256 at a time through one scratch area: the size stops growing at 256 tables."""
+    L = B.lib()
+    s1, s256, s10k = (L.bhg_scan_scratch_bytes(n) for n in (1, 256, 10000))
+    assert s1 < (2 << 20)
+    assert s256 < (256 << 20)
+    assert s10k - s256 < (1 << 20)  # only the u64 scan's per-table words still grow
 
 
 def test_no_device_means_no_context():

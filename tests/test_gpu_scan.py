@@ -144,18 +144,58 @@ def test_segment_walks_and_their_misses(codec, mode):
 
 def test_step_log_overflow_falls_back_to_the_serial_walk(codec):
     """The write pass replays the count walk's logged steps (k_tscan_logw); a table whose walk
-    takes more than TS_LOG_CAP = 4,096 steps (here ~4,300 windows of 128 KiB: a 540-MB table of
-    mixed lengths after a uniform prefix) is written by the serial walk instead.  Beside it, a
-    small mixed table takes the replay; both must match the restatement."""
+    takes more than TS_LOG_CAP = 4,096 steps is walked again to write (k_tscan<true>).  To get
+    there the segment walks must miss: the records hold values with sub-record chains (as in
+    test_segment_walks_and_their_misses), so guesses land on false chains and the stitch sends
+    the table to the serial walk, whose ~4,400 windows of 128 KiB (a ~560-MB table after a
+    uniform prefix) overflow the log.  Beside it a smaller table of the same records takes the replay
+    and one with random values the segment walks.  out_path shows which pass wrote each table."""
+    from bitalosdb_amd import _lib as B
     rng = random.Random(13)
-    chunk = b"".join(rec(rand_bytes(rng, rng.randrange(8, 40)), rand_bytes(rng, rng.randrange(100, 4000)), seq=i + 1)
-                     for i in range(500))
+    sub = lambda: b"".join(struct.pack("<III", 2, 3, 1) + b"ab" + b"xyz" for _ in range(10))
+    chunk = b"".join(rec(rand_bytes(rng, 16), sub() + rand_bytes(rng, rng.randrange(1, 300)), seq=i + 1)
+                     for i in range(2000))
     k, v = rand_bytes(rng, 32), rand_bytes(rng, 1000)
     prefix = b"".join(rec(k, v, seq=i + 1) for i in range(3000))
     reps = (540 << 20) // len(chunk) + 1
     big = prefix + chunk * reps + bytes(12)
-    small = chunk * 3 + bytes(12)
-    assert check(codec, [big, small], 0) > 500 * reps
+    small = chunk * 8 + bytes(12)  # ~5 MB: 5 segments, a missed guess among them -> the replay
+    recs = [rec(rand_bytes(rng, rng.randrange(8, 40)), rand_bytes(rng, rng.randrange(100, 4000)), seq=i + 1)
+            for i in range(300)]
+    plain = b"".join(recs * 20) + bytes(12)  # random values: the guesses hold
+    tables = [big, small, plain]
+    eh, ef, ee = expected(tables, 0)
+    src = b"".join(tables)
+    off = np.zeros(len(tables) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(b) for b in tables])
+    src_t = torch.from_numpy(np.frombuffer(src + b"\0", dtype=np.uint8).copy()).to(codec.device)
+    gh, gf, ge, gp = codec.scan_tables(src_t, off, mode=0, max_out=int(ef[-1]), paths=True)
+    codec.sync()
+    gh = gh.cpu().numpy().view(np.uint8).reshape(-1).view(O.HANDLE_DT)
+    assert (gf.cpu().numpy().view(np.uint64) == ef).all()
+    assert (ge.cpu().numpy().view(np.uint64) == ee).all()
+    assert (gh["offset"] == eh["offset"]).all() and (gh["length"] == eh["length"]).all()
+    assert gp.cpu().tolist() == [B.SCAN_PATH_SERIAL, B.SCAN_PATH_REPLAY, B.SCAN_PATH_SEGMENTS]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_many_small_tables(codec, mode):
+    """More tables than one scratch pass holds (256): the per-table counts of later passes are
+    rebased on the earlier ones' totals (k_tscan_carry).  600 small tables of mixed shapes."""
+    rng = random.Random(31)
+    tables = []
+    for t in range(600):
+        kind = t % 4
+        if kind == 0:
+            tables.append(uniform_table(rng, rng.randrange(0, 40), 16, 100))
+        elif kind == 1:
+            tables.append(b"".join(rec(rand_bytes(rng, rng.randrange(1, 30)), rand_bytes(rng, rng.randrange(1, 300)))
+                                   for _ in range(rng.randrange(0, 30))) + bytes(12))
+        elif kind == 2:
+            tables.append(b"")
+        else:
+            tables.append(uniform_table(rng, 5, 8, 40, term=False) + b"panic")
+    assert check(codec, tables, mode) > 3000
 
 
 @pytest.mark.parametrize("mode", [0, 1])
