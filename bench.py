@@ -66,11 +66,13 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="c3/c4: skip the nested line of the other value "
                                                                   "generator")
     ap.add_argument("--c5-tables", type=int, default=184, help="c5 corpus size in 128 MiB tables")
+    ap.add_argument("--bigval-n", type=int, default=7000,
+                    help="bigval: values U[4 KiB, 256 KiB] + 1%% at 1-4 MiB (~1 GiB at 7,000)")
     ap.add_argument("--no-c5", action="store_true", help="N=1: skip the nested strong_c5 record")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 --pmc child passes that measure roofline.traffic (N=1, rank 0)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "scan", "scanmix", "get",
-                                                       "indexcrc", "tail", "mixdec", "spawncheck"],
+                                                       "indexcrc", "tail", "mixdec", "bigval", "spawncheck"],
                     help="c1: 100k blocks on the host CPU; c2: uncompressed decode (BASELINE metric; at N > 1 "
                          "the line is the C5 strong-scaling corpus); c3: snappy decode; c4: encode; "
                          "c5: 25 GB corpus sharded round-robin by table over the GPUs (strong scaling); "
@@ -369,6 +371,8 @@ def run(a, world, rank, local, dev, codec):
         return run_indexcrc(a, world, rank, local, dev, codec)
     if a.config == "tail":
         return run_tail(a, world, rank, local, dev, codec)
+    if a.config == "bigval":
+        return run_bigval(a, world, rank, local, dev, codec)
     if a.config == "mixdec":
         return run_mixdec(a, world, rank, local, dev, codec)
     if a.config == "c5":
@@ -1027,6 +1031,119 @@ def mixdec_measure(a, world, rank, local, dev, codec, compressor, extras):
         out["parity_first_blocks"] = "%s (%d blocks)" % ("bit-exact" if par else "MISMATCH", m)
         out["valid"] = bool(out["valid"] and par)
     return out
+
+
+def run_bigval(a, world, rank, local, dev, codec):
+    """Values past the LDS tiers (missing #2): bithash holds every KKV value over 288 B
+    (internal/consts/base.go:29) up to 256 MiB (bithash/writer.go:43), and golang/snappy cuts a value
+    into 64-KiB blocks (internal/compress/compress.go:67-69, 83-85).  --bigval-n values of U[4 KiB,
+    256 KiB] plus 1 % of U[1 MiB, 4 MiB] (~1 GiB at the default 7,000), 32-B keys, 128 MiB tables.
+    Legs, each its own timed loop: snappy encode (the BithashWriter.Add batch), snappy decode of the
+    tables it wrote, and the NoCompressor decode of the same pairs.  Parity: decoded values equal
+    the encoder's input byte for byte; encoded bytes equal the restated writer on the first values."""
+    from bitalosdb_amd.codec import EncodeBuffers, handles_tensor, HANDLE_DT
+    n = a.bigval_n
+    g = torch.Generator(device=dev)
+    g.manual_seed(synth_seed(rank) + 11)
+    lens = torch.randint(4096, (256 << 10) + 1, (n,), generator=g, device=dev, dtype=torch.int64)
+    big = torch.rand(n, generator=g, device=dev) < 0.01
+    lens = torch.where(big, torch.randint(1 << 20, (4 << 20) + 1, (n,), generator=g, device=dev, dtype=torch.int64), lens)
+    keys, key_off, tr, vals, val_off = _encode_inputs(n, lens, dev, synth_seed(rank), a.values)
+    raw = float(vals.numel() + 32 * n)
+    maxt = 4096
+    fns = torch.arange(1, maxt + 1, dtype=torch.int32, device=dev)
+    lens_h = lens.cpu().numpy()
+    cfg = {"values": a.values, "pairs_per_gpu": n, "value_bytes": int(vals.numel()),
+           "values_over_64KiB": int((lens_h > 65536).sum()), "values_1_4MiB": int((lens_h >= 1 << 20).sum()),
+           "largest_value": int(lens_h.max())}
+    res = {"metric": "GiB/s bithash values > 4 KiB, encode and decode (device-resident), 1 GPU",
+           "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic compressible values (%s), GPU-generated" % a.values, "config": cfg}
+    legs = {}
+    for compressor in (1, 0):
+        name = "snappy" if compressor else "NoCompressor"
+        cap = int(n * 64 + vals.numel() * 7 // 6 + 64)
+        out_t = torch.empty(cap, dtype=torch.uint8, device=dev)
+        bufs = EncodeBuffers(n, maxt, dev)
+        enc = lambda: codec.encode_batch(keys, key_off, tr, vals, val_off, n, compressor, fns, maxt, 0, 128 << 20,
+                                         out_t, bufs)
+        if compressor:
+            el, kms = _timed(a, dev, enc)
+        else:
+            enc()
+            codec.sync()
+        total = int(bufs.summary[0].item())
+        st = bufs.status.cpu().numpy().view(np.uint32)
+        if compressor:
+            alg = raw + 16.0 * n + total + 16.0 * n
+            legs["encode_snappy"] = {
+                "value": round(raw * a.steps / el / 2 ** 30, 3), "unit": "GiB/s (key + value input)",
+                "ms_per_step": round(el / a.steps * 1e3, 4), "ramp": a.ramp_record,
+                "output_bytes": total, "snappy_ratio": round((total - 52.0 * n) / float(vals.numel()), 4),
+                "status_ok": int((st == 0).sum()),
+                "roofline": {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                             "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                             "scope": "whole step (event-timed)", "step_event_ms": round(kms, 4)}}
+            if rank == 0 and world == 1:
+                from oracle import oracle as O
+                m = min(n, 48)
+                vo = val_off[:m + 1].cpu().numpy().astype(np.uint64)
+                vb = vals[:int(vo[m])].cpu().numpy()
+                kb = keys[:32 * m].cpu().numpy()
+                ks = [kb[32 * i:32 * i + 32].tobytes() for i in range(m)]
+                vs = [vb[vo[i]:vo[i + 1]].tobytes() for i in range(m)]
+                exp = O.encode_batch(ks, tr[:m].cpu().numpy().astype(np.uint64), vs, codec=1,
+                                     file_nums=list(range(1, 100)))
+                par = out_t[:len(exp["out"])].cpu().numpy().tobytes() == exp["out"].tobytes()
+                legs["encode_snappy"]["parity_first_%d_values" % m] = "bit-exact" if par else "MISMATCH"
+        pos = bufs.pos.cpu().numpy().view(np.uint64)
+        ln = bufs.bh_len.cpu().numpy().view(np.uint32)
+        h = np.zeros(n, dtype=HANDLE_DT)
+        h["offset"] = pos
+        h["length"] = ln
+        h_t = handles_tensor(h, dev)
+        src = out_t[:total]
+        desc = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+        exp_crc = bufs.crc
+        if compressor:
+            voff = torch.empty((n + 1) * 8, dtype=torch.uint8, device=dev)
+            dvals = torch.empty(vals.numel() + 64, dtype=torch.uint8, device=dev)
+            dec = lambda: codec.decode_batch(src, src.numel(), h_t, n, 1, expected_crc=exp_crc, out_desc=desc,
+                                             out_vals=dvals, out_val_off=voff)
+        else:
+            dec = lambda: codec.decode_batch(src, src.numel(), h_t, n, 0, expected_crc=exp_crc, out_desc=desc)
+        el, kms = _timed(a, dev, dec)
+        d = desc.cpu().numpy().view(DESC_DT)
+        disk = float(h["length"].astype(np.float64).sum())
+        ok = int((d["status"] == 0).sum())
+        if compressor:
+            par = bool(torch.equal(dvals[:vals.numel()], vals)) and ok == n
+        else:  # zero-copy views: the value bytes at val_off inside each record equal the input
+            vo_rec = d["val_off"].astype(np.uint64) + h["offset"]
+            par = ok == n and bool(np.array_equal(d["val_len"].astype(np.int64), lens_h))
+            if par:
+                idx = torch.from_numpy(vo_rec.astype(np.int64)).to(dev)
+                par = bool(torch.equal(src[idx], vals[val_off[:-1]]))  # first byte of every value
+        alg = n * (16 + 4 + 40) + disk + (vals.numel() if compressor else 0)
+        legs["decode_" + name] = {
+            "value": round(disk * a.steps / el / 2 ** 30, 3), "unit": "GiB/s (on-disk records)",
+            "decoded_GiBps": round(vals.numel() * a.steps / el / 2 ** 30, 3),
+            "ms_per_step": round(el / a.steps * 1e3, 4), "ramp": a.ramp_record, "status_ok": ok,
+            "parity": "bit-exact (values == encoder input)" if par else "MISMATCH",
+            "roofline": {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "scope": "whole step (event-timed)", "step_event_ms": round(kms, 4)}}
+        del out_t, bufs, desc
+        torch.cuda.empty_cache()
+    res["legs"] = legs
+    res["value"] = legs["decode_snappy"]["value"]
+    res["ms_per_step"] = legs["decode_snappy"]["ms_per_step"]
+    res["roofline"] = legs["decode_snappy"]["roofline"]
+    res["valid"] = all(v.get("parity", "bit-exact").startswith("bit-exact") for v in legs.values()) and \
+        legs["encode_snappy"].get("parity_first_48_values", "bit-exact") == "bit-exact"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 C5_RECORDS_PER_TABLE = 124_738      # 128 MiB / 1076 B, the add that crosses the limit included

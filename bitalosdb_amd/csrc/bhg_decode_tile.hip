@@ -58,7 +58,10 @@ __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
 // NCH: interleaved CRC chains per 128-B window (1, 2 or 4), folded with Z_{128/NCH}.  With
 // 2 waves per SIMD and a round's loads in flight, one chain's 32 dependent steps hide behind
 // memory; every fold costs a conflicted shift-table lookup.
-template <int WPB, int NCH, int PF>
+// NB: window buffers per wave -- 2: round s+1's loads in flight while round s is absorbed (the
+// product, 8 waves per CU); 1: round s+1 is requested after round s is absorbed, the latency hidden
+// by more waves per CU instead (lab: scripts/lab/c2_r6/)
+template <int WPB, int NCH, int PF, int NB = 2>
 __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restrict__ src, uint64_t src_len,
                                                           const bhg_handle *__restrict__ handles, uint32_t n,
                                                           const uint32_t *__restrict__ expected_crc,
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
         }
     };
     uint32_t hw[33];
-    uint32_t fw[2][33];
+    uint32_t fw[NB][33];
     uint64_t wb = 0;
     uint32_t mm = 1;
     int32_t qf = 0, q0 = 0;
@@ -271,24 +274,29 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
         // ---------------- phase 2: 8 rounds; lane (rr, j) on record 8s + rr
 #pragma unroll
         for (uint32_t s = 0; s < 8; s++) {
-            const uint32_t cb = s & 1;
+            const uint32_t cb = NB == 2 ? (s & 1) : 0u;
             const uint64_t wb_c = wb;
             const uint32_t mm_c = mm;
             const int32_t qf_c = qf, q0_c = q0;
             const bool hasw_c = hasw;
-            if (s + 1 < 8) {
-                rinfo(s + 1, g, wb, mm, qf, q0, hasw);
-                if (hasw) load_win(fw[cb ^ 1], wb, qf);
-            } else if (PF != 0 && tn < ntiles) {
-                // the next tile's record heads (into hw, dead since phase 1) and / or its round-0
-                // windows (into the free buffer), in flight across this round and the stores
-                const Geo gn = geo(hn, tn * 64 + lane < n);
-                if (PF & 1) load_head_lo(hw, gn);
-                if (PF & 2) {
-                    rinfo(0, gn, wb, mm, qf, q0, hasw);
-                    if (hasw) load_win(fw[cb ^ 1], wb, qf);
+            // the next round's loads: before this round's absorb (NB 2, into the other buffer) or
+            // after it (NB 1, into the same buffer)
+            auto next_loads = [&]() {
+                if (s + 1 < 8) {
+                    rinfo(s + 1, g, wb, mm, qf, q0, hasw);
+                    if (hasw) load_win(fw[NB - 1 - cb], wb, qf);
+                } else if (PF != 0 && tn < ntiles) {
+                    // the next tile's record heads (into hw, dead since phase 1) and / or its round-0
+                    // windows (into the free buffer), in flight across this round and the stores
+                    const Geo gn = geo(hn, tn * 64 + lane < n);
+                    if (PF & 1) load_head_lo(hw, gn);
+                    if (PF & 2) {
+                        rinfo(0, gn, wb, mm, qf, q0, hasw);
+                        if (hasw) load_win(fw[NB - 1 - cb], wb, qf);
+                    }
                 }
-            }
+            };
+            if (NB == 2) next_loads();
             const uint32_t hc = __shfl(hz, 8 * s + rr, 64);
             uint32_t acc = (j == ((mm_c - 1) & 7)) ? hc : 0u;
             // every window of the round dword-aligned (records at 4-aligned offsets): no byte shifts
@@ -332,6 +340,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             acc ^= __shfl_xor(acc, 4, 64);
             const uint32_t got = __shfl(acc, 8 * (lane & 7), 64);  // record 8s + r sits on lane 8r
             if ((lane >> 3) == s) mycrc = got;
+            if (NB == 1) next_loads();
         }
         if (PF == 0) wait_loads_done();  // unconditional: see bhg_device.h
         if (valid) {

@@ -1,0 +1,136 @@
+// tile_lab.hip -- development harness (not product code): k_decode_tile variants (tile_var.hip
+// instantiations, launched directly) checked descriptor for descriptor against the product
+// library's bhg_decode_batch and timed beside it (alternating, median of iters) on BASELINE
+// configs[1]'s layout: 1M x 1,076-B records in 128 MiB tables, expected CRCs, a few bad handles.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <random>
+#include <vector>
+
+#include "../../../bitalosdb_amd/csrc/bhg_crc_tables.h"
+#include "../../../include/bithashgpu.h"
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+namespace bhg {
+template <int WPB, int NCH, int PF, int NB>
+__global__ void k_decode_tile(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *,
+                              const uint32_t *);
+}
+using namespace bhg;
+
+static std::mt19937_64 rng(12345);
+
+static void put_record(std::vector<uint8_t> &b, uint64_t off, uint32_t klen, uint32_t vlen, uint32_t fn, uint64_t seq) {
+    const uint32_t hdr[3] = {klen + 8, vlen, fn};
+    memcpy(&b[off], hdr, 12);
+    for (uint32_t i = 0; i < klen; i++) b[off + 12 + i] = (uint8_t)('a' + rng() % 26);
+    const uint64_t tr = (seq << 8) | 1;
+    memcpy(&b[off + 12 + klen], &tr, 8);
+    for (uint32_t i = 0; i < vlen; i++) b[off + 20 + klen + i] = (uint8_t)rng();
+}
+
+struct Var {
+    const char *name;
+    const void *fn;
+    int wpb;
+};
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 40;
+    const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : 1000000u;
+    bhg_ctx *ctx = bhg_create(0, 0);
+    if (!ctx) { fprintf(stderr, "no ctx\n"); return 1; }
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    hipStream_t s = (hipStream_t)bhg_stream(ctx);
+    std::vector<uint32_t> z(kZTabWords);
+    build_tile_ztab(z.data());
+    uint32_t *zt;
+    CK(hipMalloc(&zt, z.size() * 4));
+    CK(hipMemcpy(zt, z.data(), z.size() * 4, hipMemcpyHostToDevice));
+    // C2 layout
+    const uint32_t L = 1076, R = (128u << 20) / L + 1, TB = R * L + 12;
+    const uint32_t ntab = (n + R - 1) / R;
+    std::vector<uint8_t> src((uint64_t)ntab * TB, 0);
+    std::vector<bhg_handle> h(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t off = (uint64_t)(i / R) * TB + (uint64_t)(i % R) * L;
+        put_record(src, off, 32, 1024, 1 + i / R, i + 1);
+        h[i] = bhg_handle{off, L, 0};
+    }
+    h[7].length = 0;
+    h[13].length = L - 1;
+    h[35].offset = src.size();
+    const uint64_t len = src.size();
+    uint8_t *dsrc; bhg_handle *dh; uint32_t *ec; bhg_desc *o1, *o2;
+    CK(hipMalloc(&dsrc, len + 64)); CK(hipMalloc(&dh, n * 16ull)); CK(hipMalloc(&ec, n * 4ull));
+    CK(hipMalloc(&o1, n * 40ull)); CK(hipMalloc(&o2, n * 40ull));
+    CK(hipMemcpy(dsrc, src.data(), len, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dh, h.data(), n * 16ull, hipMemcpyHostToDevice));
+    if (bhg_crc32c_masked_batch(ctx, dsrc, len, dh, n, ec, s) != 0) { fprintf(stderr, "crc batch\n"); return 1; }
+    CK(hipStreamSynchronize(s));
+    { uint32_t x; CK(hipMemcpy(&x, ec + 29, 4, hipMemcpyDeviceToHost)); x ^= 1; CK(hipMemcpy(ec + 29, &x, 4, hipMemcpyHostToDevice)); }
+    auto prod = [&]() { if (bhg_decode_batch(ctx, dsrc, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
+    Var vars[] = {
+        {"nb1_w16", (const void *)k_decode_tile<16, 2, 2, 1>, 16},
+        {"nb1_w12", (const void *)k_decode_tile<12, 2, 2, 1>, 12},
+        {"nb1_w8", (const void *)k_decode_tile<8, 2, 2, 1>, 8},
+        {"nb2_w8(prod-equiv)", (const void *)k_decode_tile<8, 2, 2, 2>, 8},
+    };
+    const int nv = sizeof(vars) / sizeof(vars[0]);
+    auto launch = [&](const Var &v) {
+        const uint32_t tiles = (n + 63) / 64, need = (tiles + v.wpb - 1) / v.wpb;
+        const uint32_t grid = need < (uint32_t)cus ? need : (uint32_t)cus;
+        void *args[] = {&dsrc, (void *)&len, &dh, (void *)&n, &ec, &o2, &zt};
+        CK(hipLaunchKernel(v.fn, dim3(grid), dim3(64 * v.wpb), args, 0, s));
+    };
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    auto t1 = [&](auto fn) {
+        CK(hipEventRecord(a, s)); fn(); CK(hipEventRecord(b, s)); CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b)); return ms;
+    };
+    for (int it = 0; it < 600; it++) prod();  // clocks
+    CK(hipStreamSynchronize(s));
+    std::vector<bhg_desc> d1(n), d2(n);
+    CK(hipMemcpy(d1.data(), o1, n * 40ull, hipMemcpyDeviceToHost));
+    int fails = 0;
+    for (int k = 0; k < nv; k++) {
+        CK(hipMemset(o2, 0xee, n * 40ull));
+        launch(vars[k]);
+        CK(hipStreamSynchronize(s));
+        CK(hipGetLastError());
+        CK(hipMemcpy(d2.data(), o2, n * 40ull, hipMemcpyDeviceToHost));
+        uint32_t bad = 0;
+        for (uint32_t i = 0; i < n; i++) bad += memcmp(&d1[i], &d2[i], 40) != 0;
+        printf("%-20s mismatches %u\n", vars[k].name, bad);
+        fails += bad != 0;
+    }
+    std::vector<std::vector<float>> ts(nv + 1);
+    for (int it = 0; it < iters; it++) {
+        ts[nv].push_back(t1(prod));
+        for (int k = 0; k < nv; k++) ts[k].push_back(t1([&]() { launch(vars[k]); }));
+    }
+    const double alg = (double)n * (L + 60.0);
+    for (int k = 0; k <= nv; k++) {
+        std::sort(ts[k].begin(), ts[k].end());
+        const float med = ts[k][ts[k].size() / 2];
+        printf("%-20s median %.4f ms best %.4f  frac %.4f\n", k < nv ? vars[k].name : "product", med, ts[k][0],
+               alg / (med * 1e-3) / 8e12);
+    }
+    bhg_destroy(ctx);
+    return fails ? 1 : 0;
+}
