@@ -396,6 +396,12 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (int r = set_device(c)) return r;
     bhg::Launch L = launch_of(c, stream);
     if (codec != BHG_CODEC_SNAPPY) {
+        if (bhg::long_batch(src_len, n)) {  // long records: their CRCs by the long-record pass (bhg_longcrc.hip)
+            Scratch sc;
+            if (int r = scratch_alloc(c, L.stream, bhg::long_crc_scratch_bytes(n, src_len), sc)) return r;
+            HIP_TRY(c, bhg::launch_decode_tile(L, src, src_len, handles, n, expected_crc, out_desc, sc.base));
+            return BHG_OK;
+        }
         HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off));
         return BHG_OK;
     }

@@ -52,9 +52,21 @@ inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
                          uint32_t *lists = nullptr);
-// bhg_decode_tile.hip: the NoCompressor decode kernel
+// bhg_decode_tile.hip: the NoCompressor decode kernel.  long_scratch: null, or long_crc_scratch_bytes(n,
+// src_len) bytes -- then records longer than kLongRec are CRC'd by the long-record pass (a batch of long
+// records: see long_batch)
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                              const uint32_t *expected_crc, bhg_desc *out);
+                              const uint32_t *expected_crc, bhg_desc *out, void *long_scratch = nullptr);
+// bhg_longcrc.hip: masked CRC-32C of the records longer than kLongRec, the whole chip at once (64-KiB
+// chunks, one workgroup each), completing descriptors the LONG tile kernel left (crc 0, status unchecked)
+constexpr uint32_t kLongRec = 16384;
+// the dispatch's rule: the long-record pass runs for batches whose mean record is past this (the tile
+// kernel's own path stays for the rest: its rounds handle any length, a long record at 8 lanes)
+constexpr uint64_t kLongMean = 8192;
+inline bool long_batch(uint64_t src_len, uint32_t n) { return n != 0 && src_len > (uint64_t)n * kLongMean; }
+size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len);
+hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
+                           const uint32_t *expected_crc, bhg_desc *out, void *scratch);
 // bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
 // the shift tables it reads (Launch::stab) are built on the host once per context
 size_t stream_tab_words();

@@ -24,6 +24,11 @@
     } while (0)
 
 namespace bhg {
+template <int WPB, int NCH, int PF, int NB, int LONG>
+__global__ void k_decode_tile(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *,
+                              const uint32_t *);
+}
+namespace bhg_old {
 template <int WPB, int NCH, int PF, int NB>
 __global__ void k_decode_tile(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *,
                               const uint32_t *);
@@ -44,7 +49,7 @@ static void put_record(std::vector<uint8_t> &b, uint64_t off, uint32_t klen, uin
 struct Var {
     const char *name;
     const void *fn;
-    int wpb;
+    int wpb, nargs;
 };
 
 int main(int argc, char **argv) {
@@ -58,79 +63,120 @@ int main(int argc, char **argv) {
     hipStream_t s = (hipStream_t)bhg_stream(ctx);
     std::vector<uint32_t> z(kZTabWords);
     build_tile_ztab(z.data());
-    uint32_t *zt;
+    uint32_t *zt, *zx;
     CK(hipMalloc(&zt, z.size() * 4));
     CK(hipMemcpy(zt, z.data(), z.size() * 4, hipMemcpyHostToDevice));
-    // C2 layout
-    const uint32_t L = 1076, R = (128u << 20) / L + 1, TB = R * L + 12;
-    const uint32_t ntab = (n + R - 1) / R;
-    std::vector<uint8_t> src((uint64_t)ntab * TB, 0);
-    std::vector<bhg_handle> h(n);
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t off = (uint64_t)(i / R) * TB + (uint64_t)(i % R) * L;
-        put_record(src, off, 32, 1024, 1 + i / R, i + 1);
-        h[i] = bhg_handle{off, L, 0};
-    }
-    h[7].length = 0;
-    h[13].length = L - 1;
-    h[35].offset = src.size();
-    const uint64_t len = src.size();
-    uint8_t *dsrc; bhg_handle *dh; uint32_t *ec; bhg_desc *o1, *o2;
-    CK(hipMalloc(&dsrc, len + 64)); CK(hipMalloc(&dh, n * 16ull)); CK(hipMalloc(&ec, n * 4ull));
-    CK(hipMalloc(&o1, n * 40ull)); CK(hipMalloc(&o2, n * 40ull));
-    CK(hipMemcpy(dsrc, src.data(), len, hipMemcpyHostToDevice));
-    CK(hipMemcpy(dh, h.data(), n * 16ull, hipMemcpyHostToDevice));
-    if (bhg_crc32c_masked_batch(ctx, dsrc, len, dh, n, ec, s) != 0) { fprintf(stderr, "crc batch\n"); return 1; }
-    CK(hipStreamSynchronize(s));
-    { uint32_t x; CK(hipMemcpy(&x, ec + 29, 4, hipMemcpyDeviceToHost)); x ^= 1; CK(hipMemcpy(ec + 29, &x, 4, hipMemcpyHostToDevice)); }
-    auto prod = [&]() { if (bhg_decode_batch(ctx, dsrc, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
+    std::vector<uint32_t> x(kXTabWords);
+    build_xtab(x.data());
+    CK(hipMalloc(&zx, x.size() * 4));
+    CK(hipMemcpy(zx, x.data(), x.size() * 4, hipMemcpyHostToDevice));
+    uint32_t *zl = zx + kXLong;
     Var vars[] = {
-        {"nb1_w16", (const void *)k_decode_tile<16, 2, 2, 1>, 16},
-        {"nb1_w12", (const void *)k_decode_tile<12, 2, 2, 1>, 12},
-        {"nb1_w8", (const void *)k_decode_tile<8, 2, 2, 1>, 8},
-        {"nb2_w8(prod-equiv)", (const void *)k_decode_tile<8, 2, 2, 2>, 8},
+        {"new(src)", (const void *)k_decode_tile<8, 2, 2, 2, 0>, 8, 7},
+        {"old(HEAD)", (const void *)bhg_old::k_decode_tile<8, 2, 2, 2>, 8, 7},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
-    auto launch = [&](const Var &v) {
-        const uint32_t tiles = (n + 63) / 64, need = (tiles + v.wpb - 1) / v.wpb;
-        const uint32_t grid = need < (uint32_t)cus ? need : (uint32_t)cus;
-        void *args[] = {&dsrc, (void *)&len, &dh, (void *)&n, &ec, &o2, &zt};
-        CK(hipLaunchKernel(v.fn, dim3(grid), dim3(64 * v.wpb), args, 0, s));
-    };
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     auto t1 = [&](auto fn) {
         CK(hipEventRecord(a, s)); fn(); CK(hipEventRecord(b, s)); CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b)); return ms;
     };
-    for (int it = 0; it < 600; it++) prod();  // clocks
-    CK(hipStreamSynchronize(s));
-    std::vector<bhg_desc> d1(n), d2(n);
-    CK(hipMemcpy(d1.data(), o1, n * 40ull, hipMemcpyDeviceToHost));
     int fails = 0;
-    for (int k = 0; k < nv; k++) {
-        CK(hipMemset(o2, 0xee, n * 40ull));
-        launch(vars[k]);
+    // one data set: product vs every variant, descriptor for descriptor, then alternating timing
+    auto run_set = [&](const char *name, std::vector<uint8_t> &src, std::vector<bhg_handle> &h, int nit) {
+        const uint32_t n = (uint32_t)h.size();
+        const uint64_t len = src.size();
+        uint8_t *dsrc; bhg_handle *dh; uint32_t *ec; bhg_desc *o1, *o2;
+        CK(hipMalloc(&dsrc, len + 64)); CK(hipMalloc(&dh, n * 16ull)); CK(hipMalloc(&ec, n * 4ull));
+        CK(hipMalloc(&o1, n * 40ull)); CK(hipMalloc(&o2, n * 40ull));
+        CK(hipMemcpy(dsrc, src.data(), len, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dh, h.data(), n * 16ull, hipMemcpyHostToDevice));
+        if (bhg_crc32c_masked_batch(ctx, dsrc, len, dh, n, ec, s) != 0) { fprintf(stderr, "crc batch\n"); exit(1); }
         CK(hipStreamSynchronize(s));
-        CK(hipGetLastError());
-        CK(hipMemcpy(d2.data(), o2, n * 40ull, hipMemcpyDeviceToHost));
-        uint32_t bad = 0;
-        for (uint32_t i = 0; i < n; i++) bad += memcmp(&d1[i], &d2[i], 40) != 0;
-        printf("%-20s mismatches %u\n", vars[k].name, bad);
-        fails += bad != 0;
+        { uint32_t x; CK(hipMemcpy(&x, ec + 29, 4, hipMemcpyDeviceToHost)); x ^= 1; CK(hipMemcpy(ec + 29, &x, 4, hipMemcpyHostToDevice)); }
+        auto prod = [&]() { if (bhg_decode_batch(ctx, dsrc, len, dh, n, 0, ec, o1, nullptr, 0, nullptr, s)) { fprintf(stderr, "prod\n"); exit(1); } };
+        auto launch = [&](const Var &v) {
+            const uint32_t tiles = (n + 63) / 64, need = (tiles + v.wpb - 1) / v.wpb;
+            const uint32_t grid = need < (uint32_t)cus ? need : (uint32_t)cus;
+            void *args[] = {&dsrc, (void *)&len, &dh, (void *)&n, &ec, &o2, &zt, &zl};
+            CK(hipLaunchKernel(v.fn, dim3(grid), dim3(64 * v.wpb), args, 0, s));
+        };
+        for (int it = 0; it < 600 && it < 40 * nit; it++) prod();  // clocks
+        CK(hipStreamSynchronize(s));
+        std::vector<bhg_desc> d1(n), d2(n);
+        CK(hipMemcpy(d1.data(), o1, n * 40ull, hipMemcpyDeviceToHost));
+        uint32_t nok = 0, ncrcbad = 0;
+        for (uint32_t i = 0; i < n; i++) { nok += d1[i].status == 0; ncrcbad += d1[i].status == BHG_ST_CRC_MISMATCH; }
+        printf("[%s] n=%u ok=%u crc_mismatch=%u\n", name, n, nok, ncrcbad);
+        for (int k = 0; k < nv; k++) {
+            CK(hipMemset(o2, 0xee, n * 40ull));
+            launch(vars[k]);
+            CK(hipStreamSynchronize(s));
+            CK(hipGetLastError());
+            CK(hipMemcpy(d2.data(), o2, n * 40ull, hipMemcpyDeviceToHost));
+            uint32_t bad = 0, first = ~0u;
+            for (uint32_t i = 0; i < n; i++) if (memcmp(&d1[i], &d2[i], 40) != 0) { if (!bad) first = i; bad++; }
+            printf("  %-20s mismatches vs product %u (first %d)\n", vars[k].name, bad, (int)first);
+            fails += bad != 0;
+        }
+        std::vector<std::vector<float>> ts(nv + 1);
+        for (int it = 0; it < nit; it++) {
+            ts[nv].push_back(t1(prod));
+            for (int k = 0; k < nv; k++) ts[k].push_back(t1([&]() { launch(vars[k]); }));
+        }
+        uint64_t tot = 0;
+        for (auto &x : h) tot += x.length;
+        const double alg = (double)tot + 60.0 * n;
+        for (int k = 0; k <= nv; k++) {
+            std::sort(ts[k].begin(), ts[k].end());
+            const float med = ts[k][ts[k].size() / 2];
+            printf("  %-20s median %.4f ms best %.4f  frac %.4f  (%.1f GiB/s on disk)\n", k < nv ? vars[k].name : "product",
+                   med, ts[k][0], alg / (med * 1e-3) / 8e12, tot / (med * 1e-3) / (1u << 30));
+        }
+        fflush(stdout);
+        CK(hipFree(dsrc)); CK(hipFree(dh)); CK(hipFree(ec)); CK(hipFree(o1)); CK(hipFree(o2));
+    };
+    {  // C2 layout
+        const uint32_t L = 1076, R = (128u << 20) / L + 1, TB = R * L + 12;
+        const uint32_t ntab = (n + R - 1) / R;
+        std::vector<uint8_t> src((uint64_t)ntab * TB, 0);
+        std::vector<bhg_handle> h(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t off = (uint64_t)(i / R) * TB + (uint64_t)(i % R) * L;
+            put_record(src, off, 32, 1024, 1 + i / R, i + 1);
+            h[i] = bhg_handle{off, L, 0};
+        }
+        h[7].length = 0;
+        h[13].length = L - 1;
+        h[35].offset = src.size();
+        run_set("c2", src, h, iters);
     }
-    std::vector<std::vector<float>> ts(nv + 1);
-    for (int it = 0; it < iters; it++) {
-        ts[nv].push_back(t1(prod));
-        for (int k = 0; k < nv; k++) ts[k].push_back(t1([&]() { launch(vars[k]); }));
+    {  // long records: values of 1 B .. 3 MiB at odd offsets, a few cut short (RECORD_NIL), mostly > 16 KiB
+        const uint32_t m = 3000;
+        std::vector<uint32_t> kl(m), vl(m);
+        uint64_t tot = 7;
+        for (uint32_t i = 0; i < m; i++) {
+            kl[i] = (uint32_t)(rng() % 40);
+            const uint32_t r = (uint32_t)(rng() % 100);
+            vl[i] = r < 3 ? (uint32_t)((1u << 20) + rng() % (2u << 20)) : r < 20 ? (uint32_t)(1 + rng() % 20000)
+                                                                                : (uint32_t)(16000 + rng() % 300000);
+            tot += 20 + kl[i] + vl[i];
+        }
+        std::vector<uint8_t> src(tot + 64, 0);
+        std::vector<bhg_handle> h(m);
+        uint64_t off = 7;
+        for (uint32_t i = 0; i < m; i++) {
+            put_record(src, off, kl[i], vl[i], 9, i + 1);
+            h[i] = bhg_handle{off, 20 + kl[i] + vl[i], 0};
+            off += 20 + kl[i] + vl[i];
+        }
+        h[40].length -= 1;   // RECORD_NIL, CRC still computed
+        h[41].length = 0;
+        std::shuffle(h.begin() + 100, h.begin() + 200, rng);
+        run_set("long", src, h, 10);
     }
-    const double alg = (double)n * (L + 60.0);
-    for (int k = 0; k <= nv; k++) {
-        std::sort(ts[k].begin(), ts[k].end());
-        const float med = ts[k][ts[k].size() / 2];
-        printf("%-20s median %.4f ms best %.4f  frac %.4f\n", k < nv ? vars[k].name : "product", med, ts[k][0],
-               alg / (med * 1e-3) / 8e12);
-    }
+    (void)n;
     bhg_destroy(ctx);
     return fails ? 1 : 0;
 }

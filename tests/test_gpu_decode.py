@@ -132,6 +132,53 @@ def test_expected_crc(codec):
     assert (got["status"][::7] == O.CRC_MISMATCH).all()
 
 
+def np_bytes(g, n):
+    return g.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_long_record_batches(codec, seed):
+    """A NoCompressor batch whose mean record is past 8 KiB takes the long-record pass
+    (bhg_longcrc.hip): records over 16 KiB are CRC'd as 64-KiB chunks by the whole chip and the
+    tile kernel leaves their CRC / status to it.  Mixed with short records, odd offsets, the
+    readRecord / readData statuses, lengths at the 16-KiB, 128-B and 64-KiB edges, 1-3 MiB
+    records, and expected CRCs with some flipped."""
+    rng = random.Random(seed)
+    g = np.random.default_rng(seed)
+    vlens = [g.integers(16400, 400000) for _ in range(150)] + [g.integers(1, 16000) for _ in range(30)]
+    vlens += [(1 << 20) + int(g.integers(0, 2 << 20)) for _ in range(4)]
+    vlens += [16384 - 60, 16384 - 59, 65536 - 60, 65536 - 59, 131072 - 52, 128 * 1000 - 52, 65536 * 3 + 1]
+    rng.shuffle(vlens)
+    specs = [(rand_bytes(rng, rng.randrange(0, 48)), np_bytes(g, int(v)), rng.randrange(1 << 32)) for v in vlens]
+    src, h = make_records(rng, specs, gap_max=3)
+    h = h.copy()
+    h["length"][5] -= 1                 # RECORD_NIL (its CRC is still computed)
+    h["length"][6] = 0                  # ILLEGAL_LENGTH
+    h["offset"][7] = len(src) - 100     # INCOMPLETE
+    assert len(src) > 8192 * len(h)
+    exp0, _, _ = O.decode_batch(src, h)
+    want = exp0["crc"].copy()
+    want[::5] ^= 1
+    got, _, _ = codec.decode(src, h, expected_crc=want)
+    exp, _, _ = O.decode_batch(src, h, expected_crc=want)
+    assert_desc_equal(got, exp)
+    assert (got["status"] == O.CRC_MISMATCH).sum() > 20
+
+
+def test_long_record_pass_overflow_list(codec):
+    """Handles that overlap (the same 3-MiB record many times) give more chunks than the chunk
+    list holds (src_len / 64 KiB + n + 1): those records take the overflow walk, one workgroup
+    per record; the results must not depend on which path a record took."""
+    rng = random.Random(3)
+    g = np.random.default_rng(3)
+    src, h1 = make_records(rng, [(b"big-key", np_bytes(g, 3 << 20), 7), (b"small", b"v" * 100, 8)])
+    h = np.concatenate([np.repeat(h1[:1], 150), h1[1:], np.repeat(h1[:1], 50)])
+    h["length"][10] -= 7  # one of them RECORD_NIL
+    got, _, _ = codec.decode(src, h)
+    exp, _, _ = O.decode_batch(src, h)
+    assert_desc_equal(got, exp)
+
+
 def compressible(rng, n):
     d = rand_bytes(rng, 512)
     out = bytearray()
