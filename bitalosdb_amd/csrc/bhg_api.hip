@@ -1046,17 +1046,17 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     if (n == 0) return encode_empty(c, o, L.stream);
     if (!keys || !key_off || !trailers || !vals || !val_off || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
     const size_t lens_b = ((size_t)n + 1) * 8, vlen_b = ((size_t)n + 1) * 8, scan_b = bhg::scan_scratch_bytes(n);
-    size_t snap_b = 0, soff_b = 0, gt_b = 0, cls_b = 0;
+    size_t snap_b = 0, soff_b = 0, blk_b = 0, cls_b = 0;
     if (codec == BHG_CODEC_SNAPPY) {
         // sum MaxEncodedLen = 32 n + V + sum(v_i / 6) <= 32 n + V + V / 6 (encode.go MaxEncodedLen)
         snap_b = (size_t)(32ull * n + vals_len + vals_len / 6 + 64);
         soff_b = ((size_t)n + 1) * 8;
-        gt_b = (size_t)bhg::snappy_enc_grid(L, n) * 16384 * 2;
+        blk_b = bhg::snappy_block_scratch_bytes(n, vals_len);
         cls_b = bhg::snappy_enc_list_bytes(n);
     }
     Scratch sc;
     const size_t al6 = 6 * 256;
-    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + gt_b + cls_b + al6, sc)) return r;
+    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + blk_b + cls_b + al6, sc)) return r;
     bhg::EncodeLaunch E;
     memset(&E, 0, sizeof E);
     E.lens = reinterpret_cast<uint64_t *>(sc.take(lens_b));
@@ -1065,11 +1065,11 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     if (codec == BHG_CODEC_SNAPPY) {
         uint8_t *snap = sc.take(snap_b);
         uint64_t *soff = reinterpret_cast<uint64_t *>(sc.take(soff_b));
-        uint16_t *gt = reinterpret_cast<uint16_t *>(sc.take(gt_b));
+        void *blk = sc.take(blk_b);
         uint32_t *cls = reinterpret_cast<uint32_t *>(sc.take(cls_b));
         HIP_TRY(c, bhg::launch_snappy_maxlen(L, val_off, n, soff));
         HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, soff, soff, n, E.scan_scratch));
-        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, snap, snap_b, soff, vlen, gt, cls));
+        HIP_TRY(c, bhg::launch_snappy_enc(L, vals, val_off, n, vals_len, snap, snap_b, soff, vlen, cls, blk));
         E.vbase = snap; E.vpos = soff; E.vlen = vlen; E.vend = snap + snap_b;
     } else {
         HIP_TRY(c, bhg::launch_enc_rawvals(L, val_off, n, vlen));

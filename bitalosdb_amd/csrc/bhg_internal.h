@@ -158,11 +158,12 @@ hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_
 
 // bhg_snappy_enc.hip
 hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *out);
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n);
 size_t snappy_enc_list_bytes(uint32_t n);  // the value-class lists launch_snappy_enc needs
-hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
-                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
-                             uint16_t *gtables, uint32_t *lists);
+// the block path's scratch (values > 4 KiB: their 64-KiB blocks, each a work item)
+size_t snappy_block_scratch_bytes(uint32_t n, uint64_t vals_len);
+hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n, uint64_t vals_len,
+                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen, uint32_t *lists,
+                             void *block_scratch);
 
 // bhg_tail.hip: Writer.writeTable's tail for many tables (include/bithashgpu.h bhg_table_tail)
 struct TailLaunch {

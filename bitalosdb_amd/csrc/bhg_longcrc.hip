@@ -107,6 +107,9 @@ __global__ __launch_bounds__(256) void k_lc_emit(const uint64_t *__restrict__ ba
             for (uint64_t k = 0; k < b1 - b0; k++) ent[b0 + k] = make_uint2(i, (uint32_t)k);
         } else {
             ovf[1 + atomicAdd(ovf, 1u)] = i;
+            // the list ends inside this record (base is non-decreasing: every later record
+            // overflows too): its list slots up to cap are marked empty
+            for (uint64_t k = b0; k < cap; k++) ent[k] = make_uint2(0xffffffffu, 0u);
         }
     }
 }
@@ -161,6 +164,7 @@ __global__ __launch_bounds__(kLcThreads) void k_lc_chunk(const uint8_t *__restri
     // record completes its descriptor
     for (uint64_t g = blockIdx.x; g < nlist; g += gridDim.x) {
         const uint2 e = ent[g];
+        if (e.x == 0xffffffffu) continue;  // past the last record that fits (workgroup-uniform)
         const uint32_t v = chunk_state(e.x, e.y);
         if (t == 0) {
             const uint32_t L = h[e.x].length, nch = (uint32_t)(((uint64_t)L + kLcChunk - 1) / kLcChunk);

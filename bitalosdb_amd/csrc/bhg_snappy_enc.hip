@@ -11,8 +11,12 @@
 // and the first lane that matches (or runs past sLimit) ends the batch.
 // Table writes use ds_max_u32: positions only grow, so max == "last write
 // wins" in program order.  Match extension compares 64 bytes per step.
-// Blocks longer than 4 KiB (values > 4 KiB are cut in 64 KiB blocks) use a
-// lane-0 walk with the table in global scratch.
+// Values longer than 4 KiB (golang/snappy cuts them into 64-KiB blocks) take the block path:
+// every 64-KiB block of every such value is a work item of its own (k_snappy_enc_blocks: one
+// wave per block, block and table in LDS, the same matcher), written to a block slot; then
+// k_snappy_concat joins each value's uvarint header and block outputs.  (Until round 6 a lane-0
+// walk with its table in global memory encoded them one block after another: bench.py --config
+// bigval 764 ms per step, 1.3 GiB/s, profiles/r6/bigval/.)
 #include "bhg_device.h"
 #include "bhg_internal.h"
 
@@ -30,7 +34,8 @@ constexpr uint32_t kSeWaves = 7;   // resident waves per CU the large-value laun
 // 11 waves per CU (a u32 table: 7 waves per CU, 37.7 vs 49.4 GiB/s in round 2)
 typedef uint16_t se_tab_t;
 
-#define SE_CAP 4096                 // LDS block capacity of the large-value kernel
+#define SE_CAP 4096                 // LDS block capacity of the large-value kernel (values past it: the block path)
+#define SE_CAP_BLOCK 65536          // ... of the block path (encode.go maxBlockSize)
 #define SE_CAP_SMALL 2048           // ... of the small-value kernel (values <= 2 KiB)
 #define SE_MAXBLOCK 65536           // encode.go maxBlockSize
 #define SE_MARGIN 15                // inputMargin
@@ -41,7 +46,7 @@ typedef uint16_t se_tab_t;
 // off (no exec-mask branch)
 template <int CAP>
 struct SeLayout {
-    static constexpr uint32_t kTab = CAP;
+    static constexpr uint32_t kTab = CAP < 16384 ? CAP : 16384;  // tableSize <= min(len, maxTableSize)
     static constexpr uint32_t kDummy = kTab + 2 * kSeDcnt;
     static constexpr uint32_t kWords = (CAP + 16) / 4 + kTab * sizeof(se_tab_t) / 4 + kSeDcnt + 32;
 };
@@ -490,66 +495,17 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
     if (r.n) se_flush(o, in, r, lane);
 }
 
-// encodeBlock, lane 0 only, table of u16 in global scratch (blocks > SE_CAP)
-__device__ void se_block_serial(Out &o, const uint8_t *src, uint32_t len, uint16_t *table) {
-    uint32_t shift = 24;
-    for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
-    for (uint32_t i = 0; i < 16384; i++) table[i] = 0;
-    auto ld32 = [&](uint32_t i) {
-        return (uint32_t)src[i] | ((uint32_t)src[i + 1] << 8) | ((uint32_t)src[i + 2] << 16) | ((uint32_t)src[i + 3] << 24);
-    };
-    const int sLimit = (int)len - SE_MARGIN;
-    int nextEmit = 0, s = 1;
-    uint32_t nextHash = se_hash(ld32(1), shift);
-    for (;;) {
-        int skip = 32, nextS = s, candidate = 0;
-        for (;;) {
-            s = nextS;
-            const int b = skip >> 5;
-            nextS = s + b;
-            skip += b;
-            if (nextS > sLimit) goto rem;
-            candidate = table[nextHash & 16383];
-            table[nextHash & 16383] = (uint16_t)s;
-            nextHash = se_hash(ld32(nextS), shift);
-            if (ld32(s) == ld32(candidate)) break;
-        }
-        se_emit_literal(o, nullptr, src + nextEmit, s - nextEmit, 0, 1);
-        for (;;) {
-            const int base = s;
-            s += 4;
-            for (int i = candidate + 4; s < (int)len && src[i] == src[s]; i++, s++) {}
-            se_emit_copy(o, base - candidate, s - base, 0);
-            nextEmit = s;
-            if (s >= sLimit) goto rem;
-            const uint64_t x = (uint64_t)ld32(s - 1) | ((uint64_t)ld32(s + 3) << 32);
-            table[se_hash((uint32_t)x, shift) & 16383] = (uint16_t)(s - 1);
-            const uint32_t ch = se_hash((uint32_t)(x >> 8), shift) & 16383;
-            candidate = table[ch];
-            table[ch] = (uint16_t)s;
-            if ((uint32_t)(x >> 8) != ld32(candidate)) {
-                nextHash = se_hash((uint32_t)(x >> 16), shift);
-                s++;
-                break;
-            }
-        }
-    }
-rem:
-    if (nextEmit < (int)len) se_emit_literal(o, nullptr, src + nextEmit, len - nextEmit, 0, 1);
-}
-
 // one wave per value: val bytes vals[val_off[i] .. val_off[i+1]) -> scratch[soff[i] ..), clen[i],
 // for the values i = list[0 .. *cnt) (*head: the work-queue head, zeroed by the caller).  CAP:
 // the LDS block capacity (SE_CAP_SMALL: the values <= 2 KiB, whose 7.3 KiB of LDS lets VGPRs
-// bound the waves per CU; SE_CAP: the others, 13.2 KiB; blocks longer than CAP take the lane-0
-// path with its table in gtables).
+// bound the waves per CU; SE_CAP: the values of 2-4 KiB, 13.2 KiB).  The class lists never hold a
+// value longer than CAP (k_enc_class: longer values take the block path).
 template <int CAP, int WPG, int MINW>
 __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
                                                    const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt,
                                                    uint32_t *__restrict__ head,
                                                    uint8_t *__restrict__ scratch, uint64_t scap,
-                                                   const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen,
-                                                   uint16_t *__restrict__ gtables) {
+                                                   const uint64_t *__restrict__ soff, uint64_t *__restrict__ clen) {
     // one LDS buffer: block (+16 zero bytes), table, dedupe counters, scratch store slots.
     // The copy loop's compares read up to 67 bytes past a position < CAP: into the
     // table, never past the buffer, and clipped to the block length.
@@ -566,8 +522,6 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t j = lane; j < kSeDcnt; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
-    // the small-value launch passes no gtables: its blocks (<= SE_CAP_SMALL) always fit CAP
-    uint16_t *gt = gtables != nullptr ? gtables + (size_t)gw * 16384 : nullptr;
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef BHG_SE_PROF
     const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
@@ -658,7 +612,7 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
             const uint8_t *bs = src + b0;
             if (blen < SE_MINNONLIT) {
                 se_emit_literal(o, nullptr, bs, blen, lane);
-            } else if (blen <= (uint32_t)CAP) {
+            } else {  // blen <= CAP: the class lists hold values of at most CAP bytes
                 // one 16-B load per lane per 1 KiB (one memory round trip), then the 16 zero bytes
                 for (uint32_t t = 16 * lane; t < blen; t += 1024) {
                     u32x4 v;
@@ -680,14 +634,6 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
                 wsync();
                 hook();
                 se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
-            } else {
-                uint32_t d = o.d;
-                if (lane == 0) {
-                    Out ol = o;
-                    se_block_serial(ol, bs, blen, gt);
-                    d = ol.d;
-                }
-                o.d = uni(d);
             }
         }
         hook();  // (values with no LDS block)
@@ -722,7 +668,8 @@ hipError_t launch_snappy_maxlen(const Launch &L, const uint64_t *val_off, uint32
     return hipGetLastError();
 }
 
-// values <= SE_CAP_SMALL -> list[0 ..), the others -> list[n ..); counts in cnt[0], cnt[1]
+// values <= SE_CAP_SMALL -> list[0 ..), those of (SE_CAP_SMALL, SE_CAP] -> list[n ..) (longer ones take the
+// block path); counts in cnt[0], cnt[1]
 // (zeroed by the caller).  A workgroup of 16 waves takes 4,096 consecutive values and makes one
 // atomic per list (one per wave contended on two addresses: 0.36 ms per 1M values).  Order
 // within a list only schedules the encoder's waves.
@@ -738,8 +685,9 @@ __global__ __launch_bounds__(64 * kClassWaves) void k_enc_class(const uint64_t *
 #pragma unroll
     for (uint32_t it = 0; it < kClassPer; it++) {
         const uint32_t i = b0 + it * 64 * kClassWaves + threadIdx.x;
-        const bool v = i < n;
-        const bool big = v && val_off[i + 1] - val_off[i] > SE_CAP_SMALL;
+        const uint64_t vl = i < n ? val_off[i + 1] - val_off[i] : 0;
+        const bool v = i < n && vl <= SE_CAP;  // longer values: the block path (k_snappy_enc_blocks)
+        const bool big = v && vl > SE_CAP_SMALL;
         mb[it] = __ballot(big);
         ms[it] = __ballot(v && !big);
         cs += (uint32_t)__builtin_popcountll(ms[it]);
@@ -781,32 +729,192 @@ static uint32_t enc_grid(const Launch &L, uint32_t n) {
     return g ? g : 1;
 }
 
-// waves of the large-value launch (one global hash table each for blocks > SE_CAP)
-uint32_t snappy_enc_grid(const Launch &L, uint32_t n) { return enc_grid<SE_CAP, kSeWpg, 3>(L, n) * kSeWpg; }
+// ---- the block path: values longer than SE_CAP ----
+constexpr uint32_t kSeBlockMax = 32 + SE_MAXBLOCK + SE_MAXBLOCK / 6;  // MaxEncodedLen(64 KiB): a full block's slot
 
-// class lists (2n), class counts (4 words), then 2 x kSeHeads queue heads of 32 words each
-constexpr uint32_t kQueueWords = 4 + 2 * kSeHeads * 32;
+// per value: its 64-KiB blocks when it takes the block path (else 0), and the bytes of its block
+// slots (full blocks kSeBlockMax apart, the last one MaxEncodedLen of its length)
+// (a value past the vals_len the caller passed gets no blocks and clen ~0: NO_SPACE, as the
+// value kernels' scratch check gives)
+__global__ __launch_bounds__(256) void k_enc_bcount(const uint64_t *__restrict__ val_off, uint32_t n, uint64_t vals_len,
+                                                    uint64_t *__restrict__ bcnt, uint64_t *__restrict__ bbytes,
+                                                    uint64_t *__restrict__ clen) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t v = val_off[i + 1] - val_off[i];
+        uint64_t nb = 0, by = 0;
+        if (v > SE_CAP && val_off[i + 1] > vals_len) {
+            clen[i] = ~0ull;
+        } else if (v > SE_CAP) {
+            nb = (v + SE_MAXBLOCK - 1) / SE_MAXBLOCK;
+            const uint64_t last = v - (nb - 1) * SE_MAXBLOCK;
+            by = (nb - 1) * kSeBlockMax + 32 + last + last / 6;
+        }
+        bcnt[i] = nb;
+        bbytes[i] = by;
+    }
+}
+
+// after the scans (bbase: first block index per value, bbase[n] blocks; bsoff: slot bytes):
+// the (value, block) list
+__global__ __launch_bounds__(256) void k_enc_bemit(const uint64_t *__restrict__ bbase, uint32_t n,
+                                                   uint2 *__restrict__ ent) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t b0 = bbase[i], b1 = bbase[i + 1];
+        for (uint64_t b = b0; b < b1; b++) ent[b] = make_uint2(i, (uint32_t)(b - b0));
+    }
+}
+
+// one wave per 64-KiB block (one per CU: block + 16-K-entry table ~ 98 KiB of LDS), blocks taken
+// from a queue: encodeBlock (or emitLiteral for a last block under 17 bytes) into the block's slot,
+// its length into bclen
+__global__ __launch_bounds__(64) void k_snappy_enc_blocks(const uint8_t *__restrict__ vals,
+                                                          const uint64_t *__restrict__ val_off,
+                                                          const uint64_t *__restrict__ bbase, uint32_t n,
+                                                          const uint2 *__restrict__ ent, uint32_t *__restrict__ head,
+                                                          uint8_t *__restrict__ bscr, const uint64_t *__restrict__ bsoff,
+                                                          uint32_t *__restrict__ bclen) {
+    typedef SeLayout<SE_CAP_BLOCK> LY;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LY::kWords];
+    uint8_t *in = reinterpret_cast<uint8_t *>(lds);
+    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP_BLOCK + 16) / 4);
+    uint32_t *dcnt = lds + (SE_CAP_BLOCK + 16) / 4 + LY::kTab * sizeof(se_tab_t) / 4;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t j = lane; j < kSeDcnt; j += 64) dcnt[j] = 0;
+    const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t total = bbase[n];
+    uint32_t q = blockIdx.x;  // the first block: no queue round trip
+    while (q < total) {
+        const uint2 e = ent[q];
+        // the next block's position, taken now (its atomic in flight while this block runs)
+        uint32_t nq = 0;
+        if (lane == 0) nq = atomicAdd(head, 1u) + gridDim.x;
+        const uint64_t v0 = val_off[e.x], vlen = val_off[e.x + 1] - v0;
+        const uint64_t b0 = (uint64_t)e.y * SE_MAXBLOCK;
+        const uint32_t blen = (uint32_t)(vlen - b0 < SE_MAXBLOCK ? vlen - b0 : SE_MAXBLOCK);
+        const uint8_t *bs = vals + v0 + b0;
+        Out o;
+        o.g = bscr + bsoff[e.x] + (uint64_t)e.y * kSeBlockMax;
+        o.d = 0;
+        if (blen < SE_MINNONLIT) {
+            se_emit_literal(o, nullptr, bs, blen, lane);
+        } else {
+            for (uint32_t t = 16 * lane; t < blen; t += 1024) {
+                u32x4 v;
+                if (t + 16 <= blen) {
+                    v = gld<u32x4u>((uint64_t)(bs + t));
+                } else {
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint32_t b = 0; t + b < blen; b++) w[b >> 2] |= (uint32_t)bs[t + b] << (8 * (b & 3));
+                    v = u32x4{w[0], w[1], w[2], w[3]};
+                }
+                *reinterpret_cast<u32x4 *>(in + t) = v;
+            }
+            wsync();
+            for (uint32_t t = blen + lane; t < blen + 16; t += 64) in[t] = 0;
+            uint32_t ts = 256;
+            while (ts < 16384 && ts < blen) ts *= 2;
+            for (uint32_t t = 8 * lane; t < ts; t += 512) *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
+            wsync();
+            se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
+        }
+        if (lane == 0) bclen[q] = o.d;
+        q = uni(nq);
+        wsync();  // the next block's staging overwrites the LDS the matcher read
+    }
+}
+
+// one wave per value of the block path: uvarint(len(src)) (encode.go Encode), then its blocks'
+// outputs in order, into the value's scratch range; clen[i] = the total
+__global__ __launch_bounds__(256) void k_snappy_concat(const uint64_t *__restrict__ val_off, uint32_t n,
+                                                       const uint64_t *__restrict__ bbase, const uint8_t *__restrict__ bscr,
+                                                       const uint64_t *__restrict__ bsoff,
+                                                       const uint32_t *__restrict__ bclen, uint8_t *__restrict__ scratch,
+                                                       uint64_t scap, const uint64_t *__restrict__ soff,
+                                                       uint64_t *__restrict__ clen) {
+    const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x / 64;
+    for (uint32_t i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+        const uint64_t b0 = bbase[i], b1 = bbase[i + 1];
+        if (b0 == b1) continue;
+        if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
+            if (lane == 0) clen[i] = ~0ull;
+            continue;
+        }
+        uint8_t *d = scratch + soff[i];
+        uint64_t x = val_off[i + 1] - val_off[i];
+        uint32_t k = 0;
+        while (x >= 0x80) {
+            if (lane == 0) d[k] = (uint8_t)x | 0x80;
+            x >>= 7;
+            k++;
+        }
+        if (lane == 0) d[k] = (uint8_t)x;
+        uint64_t pos = k + 1;
+        const uint8_t *sb = bscr + bsoff[i];
+        for (uint64_t b = b0; b < b1; b++) {
+            const uint32_t len = bclen[b];
+            const uint8_t *s = sb + (b - b0) * kSeBlockMax;
+            for (uint32_t t = lane; t < len; t += 64) d[pos + t] = s[t];
+            pos += len;
+        }
+        if (lane == 0) clen[i] = pos;
+    }
+}
+
+// class lists (2n), class counts (4 words), then 2 x kSeHeads queue heads of 32 words each, then
+// the block queue's head
+constexpr uint32_t kQueueWords = 4 + 2 * kSeHeads * 32 + 32;
 size_t snappy_enc_list_bytes(uint32_t n) { return ((size_t)2 * n + kQueueWords) * 4; }
 
-hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n,
-                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen,
-                             uint16_t *gtables, uint32_t *lists) {
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+static uint64_t max_blocks(uint32_t n, uint64_t vals_len) { return vals_len / SE_MAXBLOCK + n + 1; }
+size_t snappy_block_scratch_bytes(uint32_t n, uint64_t vals_len) {
+    const uint64_t mb = max_blocks(n, vals_len);
+    return 2 * al256(((size_t)n + 1) * 8) + al256(scan_scratch_bytes(n)) + al256(mb * 8) + al256(mb * 4) +
+           al256(32 * mb + vals_len + vals_len / 6 + 64);
+}
+
+hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_t *val_off, uint32_t n, uint64_t vals_len,
+                             uint8_t *scratch, uint64_t scap, const uint64_t *soff, uint64_t *clen, uint32_t *lists,
+                             void *block_scratch) {
     uint32_t *cnt = lists + 2 * (size_t)n;  // class counts cnt[0..1], queue heads from cnt + 4
+    uint32_t *bhead = cnt + 4 + 2 * kSeHeads * 32;
     if (hipError_t e = hipMemsetAsync(cnt, 0, kQueueWords * 4, L.stream)) return e;
     const uint32_t per = 64 * kClassWaves * kClassPer;
     hipLaunchKernelGGL(k_enc_class, dim3((n + per - 1) / per), dim3(64 * kClassWaves), 0, L.stream, val_off, n, lists,
                        cnt);
     if (hipError_t e = hipGetLastError()) return e;
-    // the small-value class never reaches se_block_serial (its values, hence its blocks, are
-    // <= SE_CAP_SMALL = its LDS capacity), so it gets no global hash tables: gtables is sized for
-    // the large-value grid only (snappy_enc_grid)
     static_assert(SE_CAP_SMALL <= SE_CAP, "small-value class must fit the LDS block");
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP_SMALL, 1, kSeMinwSmall>), dim3(enc_grid<SE_CAP_SMALL, 1, kSeMinwSmall>(L, n)), dim3(64), 0, L.stream, vals,
-                       val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen, nullptr);
+                       val_off, (const uint32_t *)lists, cnt, cnt + 4, scratch, scap, soff, clen);
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((k_snappy_enc<SE_CAP, kSeWpg, 3>), dim3(enc_grid<SE_CAP, kSeWpg, 3>(L, n)), dim3(64 * kSeWpg), 0,
-                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * kSeHeads, scratch, scap, soff, clen,
-                       gtables);
+                       L.stream, vals, val_off, (const uint32_t *)lists + n, cnt + 1, cnt + 4 + 32 * kSeHeads, scratch, scap, soff, clen);
+    if (hipError_t e = hipGetLastError()) return e;
+    // the block path (values > SE_CAP): block counts -> scans -> (value, block) list -> blocks -> concat
+    uint8_t *sp = static_cast<uint8_t *>(block_scratch);
+    uint64_t *bbase = reinterpret_cast<uint64_t *>(sp);
+    sp += al256(((size_t)n + 1) * 8);
+    uint64_t *bsoff = reinterpret_cast<uint64_t *>(sp);
+    sp += al256(((size_t)n + 1) * 8);
+    void *scan = sp;
+    sp += al256(scan_scratch_bytes(n));
+    const uint64_t mb = max_blocks(n, vals_len);
+    uint2 *ent = reinterpret_cast<uint2 *>(sp);
+    sp += al256(mb * 8);
+    uint32_t *bclen = reinterpret_cast<uint32_t *>(sp);
+    sp += al256(mb * 4);
+    uint8_t *bscr = sp;
+    hipLaunchKernelGGL(k_enc_bcount, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, val_off, n, vals_len, bbase,
+                       bsoff, clen);
+    if (hipError_t e = hipGetLastError()) return e;
+    if (hipError_t e = launch_exclusive_scan_u64(L, bbase, bbase, n, scan)) return e;
+    if (hipError_t e = launch_exclusive_scan_u64(L, bsoff, bsoff, n, scan)) return e;
+    hipLaunchKernelGGL(k_enc_bemit, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, bbase, n, ent);
+    hipLaunchKernelGGL(k_snappy_enc_blocks, dim3(L.num_cus), dim3(64), 0, L.stream, vals, val_off, bbase, n, ent, bhead,
+                       bscr, bsoff, bclen);
+    hipLaunchKernelGGL(k_snappy_concat, dim3(lane_grid(L, (uint64_t)n * 64, 256)), dim3(256), 0, L.stream, val_off, n,
+                       bbase, bscr, bsoff, bclen, scratch, scap, soff, clen);
     return hipGetLastError();
 }
 

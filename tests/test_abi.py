@@ -97,8 +97,9 @@ def test_shipped_library_has_default_knobs():
     nch = _src_default("bhg_decode_tile.hip", "kTileNch")
     bpw = _src_default("bhg_snappy_dec.hip", "kSlBpw")
     slot = _src_default("bhg_snappy_dec.hip", "kSlSlot")
-    want = {
-        rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dEE" % (nch, pf)},
+    want = {  # <WPB, NCH, PF, NB = 2, LONG>: the C2 kernel and its long-record-batch twin
+        rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dELi2ELi%dEE" % (nch, pf, lg)
+                                      for lg in (0, 1)},
     }
     # the snappy LDS tiers: tier 1 in batch order, and one multi-role launch for the lists
     assert b"_ZN3bhg16k_snappy_lds_natE" in blob and b"_ZN3bhg18k_snappy_lds_multiE" in blob

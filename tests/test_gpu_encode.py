@@ -157,6 +157,45 @@ def test_encode_snappy_byte_exact(codec, seed):
         assert dv[int(doff[i]):int(doff[i + 1])].tobytes() == vals[i]
 
 
+@pytest.mark.parametrize("seed", [21, 22])
+def test_encode_snappy_block_path(codec, seed):
+    """Values past 4 KiB: every 64-KiB block is a work item of its own (k_snappy_enc_blocks),
+    then each value's uvarint header and block outputs are joined (k_snappy_concat).  Sizes at
+    the block edges (a last block of 16 bytes is emitLiteral'd, of 17 encodeBlock'd), 1-2 MiB
+    values, incompressible / compressible / periodic / zero data, small values interleaved --
+    byte-exact with the restated encoder, and decoded back on the GPU."""
+    rng = random.Random(seed)
+    g = np.random.default_rng(seed)
+    sizes = [4097, 65535, 65536, 65537, 65536 + 16, 65536 + 17, 131072, 131072 + 3, 196608 - 1,
+             (1 << 20) + 5, (2 << 20) - 77, 100, 3000, 0, 17]
+    sizes += [rng.randrange(4097, 300000) for _ in range(40)]
+    rng.shuffle(sizes)
+    n = len(sizes)
+    keys = [rb(rng, 32) for _ in range(n)]
+    vals = []
+    for i, sz in enumerate(sizes):
+        kind = i % 4
+        if kind == 0:
+            vals.append(compressible(rng, sz))
+        elif kind == 1:
+            vals.append(g.integers(0, 256, sz, dtype=np.uint8).tobytes())
+        elif kind == 2:
+            vals.append((b"0123456789abcdefXYZ" * (sz // 19 + 1))[:sz])
+        else:
+            vals.append(bytes(sz))
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    got = codec.encode(keys, tr, vals, compressor=1, file_nums=list(range(1, 50)), table_max=4 << 20)
+    exp = O.encode_batch(keys, tr, vals, codec=1, file_nums=list(range(1, 50)), table_max=4 << 20)
+    check(got, exp)
+    h = np.zeros(n, dtype=O.HANDLE_DT)
+    h["offset"] = got["pos"]
+    h["length"] = got["bh_len"]
+    desc, dv, doff = codec.decode(got["out"], h, compressor=1)
+    assert (desc["status"] == 0).all()
+    for i in range(n):
+        assert dv[int(doff[i]):int(doff[i + 1])].tobytes() == vals[i]
+
+
 @pytest.mark.parametrize("sizes", [[0], [3000], [100, 3000], [2048, 2049], [4096] * 7, [1500] * 65,
                                    [5000, 17, 2048, 4097, 0, 64]])
 def test_encode_snappy_tiny_batches(codec, sizes):
