@@ -107,6 +107,7 @@ struct bhg_ctx {
     void *h_src = nullptr; size_t h_src_cap = 0;
     void *h_aux = nullptr; size_t h_aux_cap = 0;
     void *h_vals = nullptr; size_t h_vals_cap = 0;
+    void *h_big = nullptr; size_t h_big_cap = 0;  // the snappy big-block path's scratch (host paths)
     uint32_t *ztab = nullptr;  // tile-kernel shift tables (bhg_crc_tables.h build_tile_ztab)
     uint32_t *stab = nullptr;  // stream-kernel shift tables (bhg_decode_stream.h build_stream_tab)
     uint32_t *xtab = nullptr;  // CrcR8-kernel shift tables (bhg_crc_tables.h build_xtab)
@@ -118,6 +119,8 @@ struct bhg_ctx {
     // ... the snappy pipeline's per-slot decoded values, chunk totals (page-locked) and their events
     void *pvals[kPipe] = {nullptr, nullptr, nullptr};
     size_t pvals_cap[kPipe] = {0, 0, 0};
+    void *pbig[kPipe] = {nullptr, nullptr, nullptr};  // ... per slot: the snappy big-block path's scratch
+    size_t pbig_cap[kPipe] = {0, 0, 0};
     uint64_t *ptot = nullptr;
     hipEvent_t pev[kPipe] = {nullptr, nullptr, nullptr};   // chunk total in ptot
     hipEvent_t pevb[kPipe] = {nullptr, nullptr, nullptr};  // chunk values decoded
@@ -296,6 +299,7 @@ void bhg_destroy(bhg_ctx *c) {
         if (c->pstream[k]) { (void)hipStreamSynchronize(c->pstream[k]); (void)hipStreamDestroy(c->pstream[k]); }
         if (c->pbuf[k]) (void)hipFree(c->pbuf[k]);
         if (c->pvals[k]) (void)hipFree(c->pvals[k]);
+        if (c->pbig[k]) (void)hipFree(c->pbig[k]);
         if (c->pev[k]) (void)hipEventDestroy(c->pev[k]);
         if (c->pevb[k]) (void)hipEventDestroy(c->pevb[k]);
         if (c->pevd[k]) (void)hipEventDestroy(c->pevd[k]);
@@ -307,6 +311,7 @@ void bhg_destroy(bhg_ctx *c) {
     if (c->h_src) (void)hipFree(c->h_src);
     if (c->h_aux) (void)hipFree(c->h_aux);
     if (c->h_vals) (void)hipFree(c->h_vals);
+    if (c->h_big) (void)hipFree(c->h_big);
     if (c->ztab) (void)hipFree(c->ztab);
     if (c->stab) (void)hipFree(c->stab);
     if (c->xtab) (void)hipFree(c->xtab);
@@ -408,12 +413,15 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     // snappy: the header pass also sorts the blocks into the decode lists (when values are wanted)
     Scratch sc;
     const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
-    if (int r = scratch_alloc(c, L.stream, scan_b + (out_vals ? bhg::snappy_list_bytes(n) : 0), sc)) return r;
+    const size_t list_b = out_vals ? (bhg::snappy_list_bytes(n) + 255) & ~(size_t)255 : 0;
+    const size_t big_b = out_vals ? bhg::snappy_big_bytes(n, out_vals_cap) : 0;
+    if (int r = scratch_alloc(c, L.stream, scan_b + list_b + big_b, sc)) return r;
     uint32_t *lists = out_vals ? reinterpret_cast<uint32_t *>(sc.base + scan_b) : nullptr;
     HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off, lists));
     HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
     if (out_vals)
-        HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off, lists));
+        HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off, lists,
+                                      sc.base + scan_b + list_b));
     return BHG_OK;
 }
 
@@ -672,7 +680,9 @@ int decode_host_snappy_pipelined(bhg_ctx *c, const uint8_t *src, uint64_t src_le
         uint8_t *dv = reinterpret_cast<uint8_t *>(c->pvals[ch.slot]) + ch.mis;
         const uint64_t ecap = out_vals_cap < vbase + tot ? out_vals_cap : vbase + tot;
         HIP_TRY(c, bhg::launch_add_u64(L, S.off, (uint64_t)ch.cn + 1, vbase, 1));
-        HIP_TRY(c, bhg::launch_snappy(L, S.src, ch.hi - ch.lo, S.h, ch.cn, S.d, dv - vbase, ecap, S.off, S.list));
+        if (int r = ensure_buf(c, &c->pbig[ch.slot], &c->pbig_cap[ch.slot], bhg::snappy_big_bytes(ch.cn, ecap))) return r;
+        HIP_TRY(c, bhg::launch_snappy(L, S.src, ch.hi - ch.lo, S.h, ch.cn, S.d, dv - vbase, ecap, S.off, S.list,
+                                      c->pbig[ch.slot]));
         HIP_TRY(c, hipEventRecord(c->pevb[ch.slot], sc));
         vbase += tot;
         return BHG_OK;
@@ -893,7 +903,8 @@ int bhg_decode_batch_host(bhg_ctx *c, const uint8_t *src, uint64_t src_len, cons
             if (int r = ensure_buf(c, &c->h_vals, &c->h_vals_cap, total + 80)) return r;
             uint8_t *mv = const_cast<uint8_t *>(static_cast<const uint8_t *>(mapped_device_ptr(out_vals)));
             uint8_t *dv = reinterpret_cast<uint8_t *>(c->h_vals) + (mv ? ((uintptr_t)mv & 15u) : 0u);
-            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dlist));
+            if (int r = ensure_buf(c, &c->h_big, &c->h_big_cap, bhg::snappy_big_bytes(n, total))) return r;
+            HIP_TRY(c, bhg::launch_snappy(L, dsrc, src_len, dh, n, dd, dv, total, doff, dlist, c->h_big));
             if (total && mv) HIP_TRY(c, bhg::launch_copy_out(L, dv, mv, total));
             else if (total) HIP_TRY(c, hipMemcpyAsync(out_vals, dv, total, hipMemcpyDeviceToHost, s));
         }

@@ -84,9 +84,11 @@ hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t sr
 // entries apart (small, then large in the same order), then the global-memory list (n).  A
 // header-pass tile t (64 handles) appends to sub-list t mod 64 of its class, so no sub-list takes
 // more than snappy_sub_cap(n) and the appends of ~16k tiles spread over 64 counters per class.
+// big: snappy_big_bytes(n, out_cap) bytes of scratch for the blocks past the LDS tiers (chunk-parallel)
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
-                         uint32_t *list);
+                         uint32_t *list, void *big);
+size_t snappy_big_bytes(uint32_t n, uint64_t out_cap);
 // size buckets of the 4-KiB tier, so a wave's 6 blocks walk alike (it runs as long as its longest):
 // mixdec 4.89 -> 4.28 ms with 4; 8 and 12 buckets 4.31-4.32 / 4.36-4.39 (profiles/r5/snappy_buckets)
 constexpr uint32_t kSnapBuckets = 4;

@@ -159,6 +159,93 @@ __device__ __forceinline__ bool snappy_decode_rt(uint64_t cp, uint32_t slen, uin
     return d == dlen;
 }
 
+// One CHUNK of a block (the big-block path below): the elements from stream position s0 to s_end
+// (positions after the uvarint header), writing output [d0, d_end) of the block's dlen.  The same
+// checks as snappy_decode_rt, plus: a copy reaching before d0 (into another chunk, which another lane
+// may not have written yet), an element passing s_end or d_end, or not ending exactly at (s_end,
+// d_end) -> false, and the block is decoded again serially (k_snappy_rt), which gives the exact
+// status.  (golang/snappy encodes every 64-KiB input block on its own, so its copies never reach
+// before their block, and a chunk starts at a block's first element or later.)
+__device__ __forceinline__ bool snappy_decode_chunk(uint64_t cp, uint32_t s0, uint32_t s_end, uint64_t dst, uint32_t d0,
+                                                    uint32_t d_end, uint64_t end, uint64_t oend) {
+    const uint64_t oe = dst + d_end;
+    uint32_t s = s0, d = d0;
+    auto tag8 = [&](uint64_t p) -> uint64_t { return ld64_bounded(p, end); };
+    uint64_t t8 = s < s_end ? tag8(cp + s) : 0;
+    while (s < s_end) {
+        const uint32_t tag = (uint32_t)t8 & 0xffu;
+        uint32_t n, R;
+        uint64_t A, hi;
+        bool lit;
+        if ((tag & 3) == 0) {
+            uint32_t x = tag >> 2;
+            uint64_t l64;
+            if (x < 60) {
+                s += 1;
+                l64 = (uint64_t)x + 1;
+            } else {
+                const uint32_t nb = x - 59;
+                if ((uint64_t)s + 1 + nb > s_end) return false;
+                s += 1 + nb;
+                x = (uint32_t)(t8 >> 8) & (nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u));
+                l64 = (uint64_t)x + 1;
+            }
+            if (l64 > (uint64_t)(d_end - d) || l64 > (uint64_t)(s_end - s)) return false;
+            n = (uint32_t)l64;
+            A = cp + s;
+            R = n;
+            hi = end;
+            lit = true;
+            s += n;
+        } else {
+            uint32_t offset;
+            if ((tag & 3) == 1) {
+                if ((uint64_t)s + 2 > s_end) return false;
+                s += 2;
+                n = 4 + ((tag >> 2) & 7);
+                offset = ((tag & 0xe0) << 3) | ((uint32_t)(t8 >> 8) & 0xffu);
+            } else if ((tag & 3) == 2) {
+                if ((uint64_t)s + 3 > s_end) return false;
+                s += 3;
+                n = 1 + (tag >> 2);
+                offset = (uint32_t)(t8 >> 8) & 0xffffu;
+            } else {
+                if ((uint64_t)s + 5 > s_end) return false;
+                s += 5;
+                n = 1 + (tag >> 2);
+                offset = (uint32_t)(t8 >> 8);
+            }
+            if (offset == 0 || d - d0 < offset || n > d_end - d) return false;
+            A = dst + d - offset;
+            R = offset < n ? offset : n;
+            hi = oend;
+            lit = false;
+        }
+        if (s < s_end) t8 = tag8(cp + s);
+        const uint64_t o = dst + d;
+        for (uint32_t k = 0; k < n;) {
+            const uint32_t seg = lit ? (n - k < 64u ? n - k : 64u) : n;
+            const uint64_t a = lit ? A + k : A;
+            const uint32_t rb = lit ? seg : R;
+            const u32x4 z = {0, 0, 0, 0};
+            const u32x4 c0 = ld16_hi(a, hi);
+            const u32x4 c1 = rb > 16 ? ld16_hi(a + 16, hi) : z;
+            const u32x4 c2 = rb > 32 ? ld16_hi(a + 32, hi) : z;
+            const u32x4 c3 = rb > 48 ? ld16_hi(a + 48, hi) : z;
+            for (uint32_t t = 0; t < seg; t += rb) {
+                const uint64_t q = o + k + t;
+                st16_clip(q, c0, oe);
+                if (rb > 16 && t + 16 < seg) st16_clip(q + 16, c1, oe);
+                if (rb > 32 && t + 32 < seg) st16_clip(q + 32, c2, oe);
+                if (rb > 48 && t + 48 < seg) st16_clip(q + 48, c3, oe);
+            }
+            k += seg;
+        }
+        d += n;
+    }
+    return s == s_end && d == d_end;
+}
+
 }  // namespace
 
 // list_cnt/list_ent: null (every block) or the count and block indices k_snappy_lds left
@@ -641,9 +728,206 @@ __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restri
                                 sub_cap, c_rt, e_rt);
 }
 
+// ---------------------------------------------------------------------------
+// Blocks past the LDS tiers (the global-memory list: decoded > 4 KiB, or an in-place spill):
+// chunk-parallel.  One lane walking a whole 1-4 MiB value took 170 ms for a batch of 7,000 values
+// of 4 KiB - 4 MiB (bench.py --config bigval, profiles/r6/bigval/): the step was the longest value's
+// serial walk.  Here
+//   k_sb_parse  one WAVE per listed block: a tag-only parse of its stream -- 64 positions at a time,
+//               every lane the element length and output length of a tag at its byte, then the
+//               element chain followed with v_readlane -- that cuts the block at the first element
+//               starting at or past every 64 KiB of output: chunks (stream start, output start).
+//               Blocks of <= 64 KiB are one chunk without a parse.  Anything irregular (a length
+//               past the stream, output past dlen, not ending exactly at the stream end) sends the
+//               block to the serial pass.
+//   k_sb_walk   LANE per chunk: snappy_decode_chunk.  The last chunk of a block (a device-scope
+//               counter per block) finalises its descriptor, or lists the block for the serial pass
+//               when any of its chunks failed (a copy into an earlier chunk, a corrupt element).
+//   k_snappy_rt the serial pass over that list (exact golang/snappy statuses).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSbChunk = 65536;  // decoded bytes per chunk (at least: a chunk starts at an element)
+struct SbEnt {
+    uint32_t i, s0, d0, last;  // block, stream start (after the uvarint header), output start; ~0 = unused slot
+};
+// layout of the big path's scratch: [0] chunk entries reserved, [1] serial list size; from 256 B the
+// entries (cap), the per-block words {chunks left, failed} (n), the serial list (n)
+static size_t al256_(size_t x) { return (x + 255) & ~(size_t)255; }
+static uint64_t sb_cap(uint32_t n, uint64_t out_cap) { return out_cap / kSbChunk + n + 1; }
+size_t snappy_big_bytes(uint32_t n, uint64_t out_cap) {
+    return 256 + al256_(sb_cap(n, out_cap) * sizeof(SbEnt)) + al256_((size_t)n * 8) + al256_((size_t)n * 4);
+}
+struct SbScratch {
+    uint32_t *ctr;
+    SbEnt *ent;
+    uint32_t *blk, *ser;
+    uint64_t cap;
+};
+static SbScratch sb_layout(void *p, uint32_t n, uint64_t out_cap) {
+    SbScratch S;
+    uint8_t *b = static_cast<uint8_t *>(p);
+    S.ctr = reinterpret_cast<uint32_t *>(b);
+    S.cap = sb_cap(n, out_cap);
+    S.ent = reinterpret_cast<SbEnt *>(b + 256);
+    S.blk = reinterpret_cast<uint32_t *>(b + 256 + al256_(S.cap * sizeof(SbEnt)));
+    S.ser = S.blk + al256_((size_t)n * 8) / 4;
+    return S;
+}
+
+constexpr uint32_t kSbBuf = 4096;  // staged stream bytes per wave (+ 128 of look-ahead)
+__global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                  const bhg_handle *__restrict__ handles, uint32_t n,
+                                                  bhg_desc *__restrict__ out, uint64_t out_cap,
+                                                  const uint64_t *__restrict__ val_off,
+                                                  const uint32_t *__restrict__ rt_cnt, const uint32_t *__restrict__ rt_ent,
+                                                  uint32_t *__restrict__ ctr, SbEnt *__restrict__ ent, uint64_t cap,
+                                                  uint32_t *__restrict__ blk, uint32_t *__restrict__ ser) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[4][kSbBuf + 128];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t *buf = bufs[w];
+    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint32_t cnt = *rt_cnt;
+    for (uint32_t j = blockIdx.x * 4 + w; j < cnt; j += gridDim.x * 4) {
+        const uint32_t i = rt_ent[j];
+        uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
+        const uint32_t status = dw[9];
+        if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
+        const uint32_t cpos = dw[2], dlen = dw[3];
+        const uint64_t o0 = val_off[i], o1 = val_off[i + 1];
+        if (o1 > out_cap || o1 - o0 < dlen) {  // as k_snappy_rt
+            if (lane == 0) { dw[2] = 0; dw[3] = 0; dw[9] = BHG_ST_SNAPPY_TOO_LARGE; }
+            continue;
+        }
+        const bhg_handle hh = handles[i];
+        const uint64_t cp = base + hh.offset + cpos;
+        const uint32_t clen = hh.length - cpos;
+        uint32_t hdr = 0;
+        while (hdr < 10 && gld<uint8_t>(cp + hdr) >= 0x80) hdr++;  // uvarint decodedLen (validated by the header pass)
+        hdr++;
+        const uint64_t S = cp + hdr;
+        const uint32_t slen = clen - hdr;
+        // chunk slots: at most one per 64 KiB of output, plus the first
+        const uint32_t k = dlen / kSbChunk + 1;
+        uint32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(ctr, k);
+        b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+        if ((uint64_t)b0 + k > cap) {  // (cannot happen: the chunks of all blocks fit out_cap / 64 KiB + n)
+            if (lane == 0) ser[atomicAdd(ctr + 1, 1u)] = i;
+            for (uint32_t q = lane; (uint64_t)b0 + q < cap && q < k; q += 64) ent[b0 + q] = SbEnt{~0u, 0, 0, 0};
+            continue;
+        }
+        uint32_t ci = 1;
+        bool bad = false;
+        if (dlen > kSbChunk) {
+            uint32_t e = 0, d = 0, nextb = kSbChunk, bb = ~0u;
+            while (e < slen) {
+                if (bb == ~0u || e + 64 + 8 > bb + kSbBuf) {  // restage [e, e + kSbBuf + 128) (bytes past the stream: 0)
+                    bb = e;
+                    sl_wsync();
+                    for (uint32_t t = 16 * lane; t < kSbBuf + 128; t += 1024) {
+                        u32x4 v = {0, 0, 0, 0};
+                        if ((uint64_t)bb + t + 16 <= slen) v = gld<u32x4u>(S + bb + t);
+                        else if (bb + t < slen) v = ld16_hi(S + bb + t, S + slen);
+                        *reinterpret_cast<u32x4_lds_u *>(buf + t) = v;
+                    }
+                    sl_wsync();
+                }
+                // lane: the element a tag at e + lane would be (elen 0: its length bytes pass the stream)
+                const uint32_t p = e + lane, x = p - bb;
+                uint32_t elen = 0, olen = 0;
+                if (p < slen) {
+                    const uint32_t tag = buf[x], ty = tag & 3u, v = tag >> 2;
+                    if (ty == 0) {
+                        uint32_t ln = v + 1, nb = 0;
+                        if (v >= 60) {
+                            nb = v - 59;
+                            uint32_t lv = 0;
+                            for (uint32_t q = 0; q < 4; q++) lv |= q < nb ? (uint32_t)buf[x + 1 + q] << (8 * q) : 0u;
+                            ln = lv + 1;  // 0 for a 4-byte 2^32 - 1: caught as irregular (ln > dlen)
+                        }
+                        const uint64_t el = 1ull + nb + ln;
+                        if (p + 1 + nb <= slen && ln != 0 && ln <= dlen && p + el <= slen) { elen = (uint32_t)el; olen = ln; }
+                    } else {
+                        const uint32_t el = ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+                        if (p + el <= slen) { elen = el; olen = ty == 1 ? 4 + (v & 7) : 1 + v; }
+                    }
+                }
+                uint32_t q = 0;
+                while (q < 64 && e + q < slen) {
+                    const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)elen, (int)q);
+                    const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)olen, (int)q);
+                    if (el == 0 || ol > dlen - d) { bad = true; break; }
+                    if (d >= nextb) {
+                        if (lane == 0) ent[b0 + ci] = SbEnt{i, e + q, d, 0};
+                        ci++;
+                        nextb = (d / kSbChunk + 1) * kSbChunk;
+                    }
+                    d += ol;
+                    q += el;
+                }
+                if (bad) break;
+                e += q;
+            }
+            if (!bad && (e != slen || d != dlen)) bad = true;
+        }
+        if (bad) {
+            for (uint32_t q = lane; q < k; q += 64) ent[b0 + q] = SbEnt{~0u, 0, 0, 0};
+            if (lane == 0) ser[atomicAdd(ctr + 1, 1u)] = i;
+            continue;
+        }
+        for (uint32_t q = ci + lane; q < k; q += 64) ent[b0 + q] = SbEnt{~0u, 0, 0, 0};
+        if (lane == 0) {
+            ent[b0] = SbEnt{i, 0, 0, ci == 1 ? 1u : 0u};
+            if (ci > 1) ent[b0 + ci - 1].last = 1;
+            blk[2 * i] = ci;
+            blk[2 * i + 1] = 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sb_walk(const uint8_t *__restrict__ src, uint64_t src_len,
+                                                 const bhg_handle *__restrict__ handles, bhg_desc *__restrict__ out,
+                                                 uint8_t *__restrict__ out_vals, uint64_t out_cap,
+                                                 const uint64_t *__restrict__ val_off, uint32_t *__restrict__ ctr,
+                                                 const SbEnt *__restrict__ ent, uint64_t cap, uint32_t *__restrict__ blk,
+                                                 uint32_t *__restrict__ ser) {
+    const uint64_t base = (uint64_t)src, end = base + src_len, oend = (uint64_t)out_vals + out_cap;
+    const uint64_t total = *ctr < cap ? *ctr : cap;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+        const SbEnt E = ent[g];
+        if (E.i == ~0u) continue;
+        const uint32_t i = E.i;
+        uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
+        const uint32_t cpos = dw[2], dlen = dw[3];
+        const bhg_handle hh = handles[i];
+        const uint64_t cp = base + hh.offset + cpos;
+        const uint32_t clen = hh.length - cpos;
+        uint32_t hdr = 0;
+        while (hdr < 10 && gld<uint8_t>(cp + hdr) >= 0x80) hdr++;
+        hdr++;
+        uint32_t s_end = clen - hdr, d_end = dlen;
+        if (!E.last) {
+            const SbEnt N = ent[g + 1];
+            s_end = N.s0;
+            d_end = N.d0;
+        }
+        const bool ok = snappy_decode_chunk(cp + hdr, E.s0, s_end, (uint64_t)out_vals + val_off[i], E.d0, d_end, end, oend);
+        if (!ok) atomicOr(blk + 2 * i + 1, 1u);
+        __threadfence();
+        if (atomicSub(blk + 2 * i, 1u) == 1u) {  // the block's last chunk
+            __threadfence();
+            if (atomicOr(blk + 2 * i + 1, 0u) == 0u) {
+                dw[2] = 0;  // the value's offset in out_vals is out_val_off[i]; status stays OK / CRC_MISMATCH
+                dw[3] = dlen;
+            } else {
+                ser[atomicAdd(ctr + 1, 1u)] = i;
+            }
+        }
+    }
+}
+
 hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
-                         uint32_t *list) {
+                         uint32_t *list, void *big) {
     if (src_len >= 64 && list) {
         // the lists the header pass filled (launch_decode with the same pointer; layout in
         // bhg_internal.h): the <= 1-KiB class, the 1-4 KiB class, and the global-memory list
@@ -667,10 +951,16 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
                                out_cap, val_off, list, cap);
             if (hipError_t e = hipGetLastError()) return e;
         }
-        // then the blocks the tiers handed on (too big for a slot, or an in-place spill), lane per
-        // block from global memory
+        // then the blocks the tiers handed on (too big for a slot, or an in-place spill): chunk-parallel
+        // (k_sb_parse, k_sb_walk), and lane per block from global memory for the ones that need it
+        const SbScratch B = sb_layout(big, n, out_cap);
+        if (hipError_t e = hipMemsetAsync(B.ctr, 0, 8, L.stream)) return e;
+        hipLaunchKernelGGL(k_sb_parse, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, n, out, out_cap,
+                           val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt, B.ctr, B.ent, B.cap, B.blk, B.ser);
+        hipLaunchKernelGGL(k_sb_walk, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, out, out_vals, out_cap,
+                           val_off, B.ctr, B.ent, B.cap, B.blk, B.ser);
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
-                           out_cap, val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt);
+                           out_cap, val_off, (const uint32_t *)(B.ctr + 1), (const uint32_t *)B.ser);
         return hipGetLastError();
     }
     uint32_t grid = (n + 255) / 256;

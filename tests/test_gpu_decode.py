@@ -298,6 +298,67 @@ def _lit(data):
     return bytes([61 << 2]) + (n - 1).to_bytes(2, "little") + data
 
 
+def _lit_any(data):
+    """emitLiteral for any length (1-4 length bytes)."""
+    n = len(data) - 1
+    if n < 60:
+        return bytes([n << 2]) + data
+    nb = (n.bit_length() + 7) // 8
+    return bytes([(59 + nb) << 2]) + n.to_bytes(nb, "little") + data
+
+
+def _copy2(off, ln):
+    return bytes([(ln - 1) << 2 | 2]) + off.to_bytes(2, "little")
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_snappy_big_blocks_chunked(codec, seed):
+    """Blocks past the LDS tiers decode chunk-parallel: a wave parses the tags and cuts the block at
+    every 64 KiB of output (k_sb_parse), a lane walks each chunk (k_sb_walk); irregular blocks fall
+    to the serial pass.  Golang-encoded values of 5 KiB - 3 MiB (compressible, random, zeros),
+    hand-built streams whose copies reach back across a 64-KiB output boundary (valid snappy the
+    chunked walk cannot decode: serial pass), a literal longer than 64 KiB with a 3-byte length, and
+    corrupted big streams -- statuses, offsets and values equal the restated decoder's."""
+    rng = random.Random(seed)
+    g = np.random.default_rng(seed)
+    vals = []
+    for i in range(60):
+        sz = rng.choice([5000, 70000, 65536, 65537, 131072 + 9, 300000, (1 << 20) + 7, 3 << 20])
+        k = i % 3
+        vals.append(compressible(rng, sz) if k == 0 else g.integers(0, 256, sz, dtype=np.uint8).tobytes()
+                    if k == 1 else bytes(sz))
+    streams = [O.snappy_encode(v) for v in vals]
+    big = g.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    cross = _lit_any(big) + _copy2(30000, 64) * 100 + _copy2(1, 60)  # copies from 30 KB back at d >= 64 KiB
+    streams.append(_uvarint(70000 + 6400 + 60) + cross)
+    lit3 = _lit_any(big + big[:1000])                              # one literal of 71,000 B (3-byte length)
+    streams.append(_uvarint(71000) + lit3 + _copy2(71000 % 65536, 40))
+    streams[-1] = _uvarint(71040) + lit3 + _copy2(5000, 40)
+    bad = bytearray(O.snappy_encode(compressible(rng, 500000)))
+    bad[len(bad) // 2] ^= 0xff                                     # corrupted big stream
+    streams.append(bytes(bad))
+    trunc = O.snappy_encode(compressible(rng, 200000))
+    streams.append(trunc[:-7])                                     # truncated: ends early
+    small = [O.snappy_encode(compressible(rng, rng.choice([16, 500, 1024, 3000]))) for _ in range(200)]
+    allst = streams + small
+    rng.shuffle(allst)
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(allst):
+        rec = O.record_set(b"big%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    ok = np.nonzero(exp["status"] == 0)[0]
+    assert len(ok) >= len(allst) - 3
+    for i in ok:
+        assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
+
+
 def test_snappy_long_streams_in_lds(codec):
     """Streams longer than the 64 chunks a lane-per-chunk staging covers (1,025 .. 1,064 B
     for a <= 1 KiB value: values snappy cannot shrink) are decoded in their LDS slot, the
