@@ -845,12 +845,39 @@ __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ sr
                             ln = lv + 1;  // 0 for a 4-byte 2^32 - 1: caught as irregular (ln > dlen)
                         }
                         const uint64_t el = 1ull + nb + ln;
-                        if (p + 1 + nb <= slen && ln != 0 && ln <= dlen && p + el <= slen) { elen = (uint32_t)el; olen = ln; }
+                        // (a literal past 64 MiB -- never golang/snappy's, its blocks are 64 KiB -- is left
+                        // to the serial pass, so that a window's output sum cannot wrap)
+                        if (p + 1 + nb <= slen && ln != 0 && ln <= dlen && ln <= (1u << 26) && p + el <= slen) {
+                            elen = (uint32_t)el;
+                            olen = ln;
+                        }
                     } else {
                         const uint32_t el = ty == 1 ? 2u : ty == 2 ? 3u : 5u;
                         if (p + el <= slen) { elen = el; olen = ty == 1 ? 4 + (v & 7) : 1 + v; }
                     }
                 }
+                // the chain from e through the window by pointer doubling (ds_bpermute): lane b ends at
+                // nx = the position after 2^k elements from e + b (saturating at the first one past the
+                // window), sm = their output; 5 levels cover the <= 32 elements of 64 bytes (an element is
+                // >= 2 bytes).  Positions past the stream are fixed points; 0x10000: an irregular element.
+                uint32_t nx = p >= slen ? lane : (elen ? lane + elen : 0x10000u), sm = olen;
+#pragma unroll
+                for (int lv = 0; lv < 6; lv++) {
+                    const bool in = nx < 64;
+                    const int a = (int)((in ? nx : 0u) * 4u);
+                    const uint32_t nn = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)nx);
+                    const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)sm);
+                    if (in) { nx = nn; sm += ns; }
+                }
+                const uint32_t wx = (uint32_t)__builtin_amdgcn_readfirstlane((int)nx);
+                const uint32_t ws = (uint32_t)__builtin_amdgcn_readfirstlane((int)sm);
+                if (wx >= 0x10000u || ws > dlen - d) { bad = true; break; }
+                if (d + ws < nextb) {  // no chunk boundary in this window (the common case)
+                    d += ws;
+                    e += wx;
+                    continue;
+                }
+                // a chunk boundary: the window's elements one by one
                 uint32_t q = 0;
                 while (q < 64 && e + q < slen) {
                     const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)elen, (int)q);
