@@ -77,13 +77,28 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     const Crc4Perm crc(T);
     const uint32_t lane = threadIdx.x & 63, rr = lane >> 3, j = lane & 7;
     const uint64_t base = (uint64_t)src, end = base + src_len;
-    const uint32_t ntiles = (n + 63) / 64;
-    const uint32_t tstride = gridDim.x * WPB;
-    // wave-major tile index: the waves that take one tile more than the others
-    // (ntiles mod tstride of them) are spread over every CU, not packed on the first ones
-    uint32_t tile = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    // Tiles: KF full layers of W tiles of 64 records (W waves; wave w takes tile k W + w of layer
+    // k, wave-major, so all waves sweep one region of the batch together), then ONE tail layer: the
+    // remaining R < 64 W records split evenly, a partial tile of R / W (+1) records per wave.  With
+    // whole tiles for the tail, 37 % of the waves had one tile fewer at C2 (15,625 tiles, 2,048 waves)
+    // and the launch ran as long as 8 tiles: ~7 + 30 us per tile and wave at 1..16 tiles per wave.
+    // (Contiguous per-wave ranges instead ran 3-4 % slower: profiles/r6/c2_lab/.)
+    const uint32_t W = gridDim.x * WPB, wid = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const uint32_t KF = n / (64 * W), tail0 = KF * 64 * W, pt = (n - tail0) / W, rt = (n - tail0) % W;
+    // tile k of this wave: first record and record count (0: no more tiles)
+    auto tile_at = [&](uint32_t k, uint32_t &b, uint32_t &c) {
+        if (k < KF) {
+            b = (k * W + wid) * 64;
+            c = 64;
+        } else {
+            b = tail0 + wid * pt + (wid < rt ? wid : rt);
+            c = k == KF ? pt + (wid < rt ? 1u : 0u) : 0u;
+        }
+    };
+    uint32_t tk = 0, tile, tcnt;
+    tile_at(0, tile, tcnt);
     bhg_handle hn = {0, 0, 0};
-    if (tile < ntiles && tile * 64 + lane < n) hn = handles[tile * 64 + lane];
+    if (lane < tcnt) hn = handles[tile + lane];
     // a record's geometry from its handle: Reader.readData's checks (reader.go:234-258), the
     // window count m = ceil(L / 128) and the head length hl = L - 128 (m-1) in 1..128
     struct Geo {
@@ -173,8 +188,8 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
     uint32_t mm = 1;
     int32_t qf = 0, q0 = 0;
     bool hasw = false;
-    if (PF != 0 && tile < ntiles) {  // the first tile's prefetched part; later tiles' come from round 7
-        const Geo g0 = geo(hn, tile * 64 + lane < n);
+    if (PF != 0 && tcnt != 0) {  // the first tile's prefetched part; later tiles' come from round 7
+        const Geo g0 = geo(hn, lane < tcnt);
         if (PF & 1) load_head_lo(hw, g0);
         if (PF & 2) {
             rinfo(0, g0, wb, mm, qf, q0, hasw);
@@ -195,13 +210,14 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             if (threadIdx.x + r * NT < kZTabWords) Z[threadIdx.x + r * NT] = v[r];
     }
     __syncthreads();
-    for (; tile < ntiles; tile += tstride) {
+    while (tcnt != 0) {
         // ---------------- phase 1: lane = record (Reader.readData's checks, readRecord, readKV)
         const bhg_handle h = hn;
-        const uint32_t i = tile * 64 + lane;
-        const uint32_t tn = tile + tstride;
-        if (tn < ntiles && tn * 64 + lane < n) hn = handles[tn * 64 + lane];
-        const bool valid = i < n;
+        const uint32_t i = tile + lane;
+        uint32_t tn, tncnt;
+        tile_at(tk + 1, tn, tncnt);
+        if (lane < tncnt) hn = handles[tn + lane];
+        const bool valid = lane < tcnt;
         // requested here, used after phase 2: a load issued at the end would expose its latency per tile
         const uint32_t ecrc = (expected_crc != nullptr && valid) ? expected_crc[i] : 0u;
         const Geo g = geo(h, valid);
@@ -289,10 +305,10 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
                 if (s + 1 < 8) {
                     rinfo(s + 1, g, wb, mm, qf, q0, hasw);
                     if (hasw) load_win(fw[NB - 1 - cb], wb, qf);
-                } else if (PF != 0 && tn < ntiles) {
+                } else if (PF != 0 && tncnt != 0) {
                     // the next tile's record heads (into hw, dead since phase 1) and / or its round-0
                     // windows (into the free buffer), in flight across this round and the stores
-                    const Geo gn = geo(hn, tn * 64 + lane < n);
+                    const Geo gn = geo(hn, lane < tncnt);
                     if (PF & 1) load_head_lo(hw, gn);
                     if (PF & 2) {
                         rinfo(0, gn, wb, mm, qf, q0, hasw);
@@ -370,6 +386,9 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             __builtin_nontemporal_store((uint64_t)dfn | ((uint64_t)dfnv << 32), o + 3);
             __builtin_nontemporal_store((uint64_t)dcrc | ((uint64_t)dst << 32), o + 4);
         }
+        tk++;
+        tile = tn;
+        tcnt = tncnt;
     }
 }
 

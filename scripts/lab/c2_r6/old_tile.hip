@@ -61,8 +61,12 @@ __device__ __forceinline__ uint32_t zapply(const uint32_t *Zt, uint32_t c) {
 // memory; every fold costs a conflicted shift-table lookup.
 // NB: window buffers per wave -- 2: round s+1's loads in flight while round s is absorbed (the
 // product, 8 waves per CU); 1: round s+1 is requested after round s is absorbed, the latency hidden
-// by more waves per CU instead (lab: scripts/lab/c2_r6/)
-template <int WPB, int NCH, int PF, int NB = 2>
+// by more waves per CU instead (lab: scripts/lab/c2_r6/, no gain).
+// LONG: records longer than kLongRec get no CRC here -- their descriptors are written with crc 0
+// and an unchecked status, and the long-record pass (bhg_longcrc.hip) computes the CRC with the
+// whole chip and completes them.  The dispatch picks LONG = 1 for batches of long records only
+// (launch_decode_tile), so the C2 instantiation is the same code as before.
+template <int WPB, int NCH, int PF, int NB = 2, int LONG = 0>
 __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restrict__ src, uint64_t src_len,
                                                           const bhg_handle *__restrict__ handles, uint32_t n,
                                                           const uint32_t *__restrict__ expected_crc,
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
         mm = __shfl(g.m, sl, 64);
         wb = pr + (Lr - 128 * (mm - 1));  // start of window 1
         q0 = (int32_t)(mm - 1) - (int32_t)j;
-        hasw = Lr != 0 && q0 >= 1;
+        hasw = Lr != 0 && q0 >= 1 && !(LONG && Lr > kLongRec);
         qf = q0 >= 1 ? (int32_t)(((uint32_t)q0 - 1) % 8 + 1) : 0;
     };
     auto load_win = [&](uint32_t *w, uint64_t wb, int32_t q) {
@@ -348,11 +352,11 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
             uint32_t dk = 0, dkl = 0, dvo = 0, dvl = 0, dfn = 0, dfnv = 0, dcrc = 0, dst = st;
             uint64_t dtr = 0;
             if (inb) {
-                dcrc = crc_mask(~mycrc);  // crc.go:31-33
+                dcrc = (LONG && L > kLongRec) ? 0u : crc_mask(~mycrc);  // crc.go:31-33 (long: the pass's)
                 if (rvalid) {
                     dk = 12; dkl = key_len; dvo = 12 + k; dvl = v;  // noCompressor.Decode: zero-copy view
                     dtr = trailer; dfn = fn; dfnv = fnv;
-                    if (expected_crc != nullptr && ecrc != dcrc) dst = BHG_ST_CRC_MISMATCH;
+                    if (expected_crc != nullptr && ecrc != dcrc && !(LONG && L > kLongRec)) dst = BHG_ST_CRC_MISMATCH;
                 } else {
                     dst = BHG_ST_RECORD_NIL;  // ErrBhReadRecordNil
                 }
@@ -371,16 +375,22 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_tile(const uint8_t *__restr
 }
 
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                              const uint32_t *expected_crc, bhg_desc *out) {
+                              const uint32_t *expected_crc, bhg_desc *out, void *long_scratch) {
     constexpr int WPB = 8;  // measured: 12 waves/CU (3 per SIMD) 0.293 ms vs 0.285; non-temporal window loads 0.58 ms
     const uint64_t tiles = (n + 63) / 64;
     uint64_t need = (tiles + WPB - 1) / WPB;
     uint64_t cap = (uint64_t)L.num_cus;  // 148 KiB of LDS: one workgroup per CU
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_tile<WPB, kTileNchOld, kTilePfOld>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len, h, n,
-                       expected_crc, out, L.ztab);
-    return hipGetLastError();
+    if (long_scratch == nullptr) {
+        hipLaunchKernelGGL((k_decode_tile<WPB, kTileNchOld, kTilePfOld>), dim3(grid), dim3(64 * WPB), 0, L.stream, src, src_len,
+                           h, n, expected_crc, out, L.ztab);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_decode_tile<WPB, kTileNchOld, kTilePfOld, 2, 1>), dim3(grid), dim3(64 * WPB), 0, L.stream, src,
+                       src_len, h, n, expected_crc, out, L.ztab);
+    if (hipError_t e = hipGetLastError()) return e;
+    return launch_long_crc(L, src, src_len, h, n, expected_crc, out, long_scratch);
 }
 
 }  // namespace bhg

@@ -29,7 +29,7 @@ __global__ void k_decode_tile(const uint8_t *, uint64_t, const bhg_handle *, uin
                               const uint32_t *);
 }
 namespace bhg_old {
-template <int WPB, int NCH, int PF, int NB>
+template <int WPB, int NCH, int PF, int NB, int LONG>
 __global__ void k_decode_tile(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *,
                               const uint32_t *);
 }
@@ -73,7 +73,7 @@ int main(int argc, char **argv) {
     uint32_t *zl = zx + kXLong;
     Var vars[] = {
         {"new(src)", (const void *)k_decode_tile<8, 2, 2, 2, 0>, 8, 7},
-        {"old(HEAD)", (const void *)bhg_old::k_decode_tile<8, 2, 2, 2>, 8, 7},
+        {"old(HEAD)", (const void *)bhg_old::k_decode_tile<8, 2, 2, 2, 0>, 8, 7},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipEvent_t a, b;

@@ -6,5 +6,5 @@ namespace bhg {
 template __global__ void k_decode_tile<8, 2, 2, 2, 0>(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *, const uint32_t *);
 }
 namespace bhg_old {
-template __global__ void k_decode_tile<8, 2, 2, 2>(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *, const uint32_t *);
+template __global__ void k_decode_tile<8, 2, 2, 2, 0>(const uint8_t *, uint64_t, const bhg_handle *, uint32_t, const uint32_t *, bhg_desc *, const uint32_t *);
 }
