@@ -35,7 +35,7 @@ if [ -n "$BENCH" ]; then
   done <<< "$BENCH"
 fi
 if [ -n "$PROF" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py $PROF > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py $PROF > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
   find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
   head -12 $O/kernel_stats.csv | cut -c1-200
 fi
