@@ -13,7 +13,7 @@
 // wins" in program order.  Match extension compares 64 bytes per step.
 // Values longer than 4 KiB (golang/snappy cuts them into 64-KiB blocks) take the block path:
 // every 64-KiB block of every such value is a work item of its own (k_snappy_enc_blocks: one
-// wave per block, block and table in LDS, the same matcher), written to a block slot; then
+// wave per block, its table in LDS, the block read in place, the same matcher), written to a block slot; then
 // k_snappy_concat joins each value's uvarint header and block outputs.  (Until round 6 a lane-0
 // walk with its table in global memory encoded them one block after another: bench.py --config
 // bigval 764 ms per step, 1.3 GiB/s, profiles/r6/bigval/.)
@@ -44,11 +44,13 @@ typedef uint16_t se_tab_t;
 // entries: tableSize <= len), the dedupe counters, and 64 scratch u16 slots (SE_DUMMY, after
 // the table and the counters): lanes that must not store write there instead of being masked
 // off (no exec-mask branch)
-template <int CAP>
+// (GSRC: the block is not staged, the matcher reads the value in place: no block words)
+template <int CAP, bool GSRC = false>
 struct SeLayout {
     static constexpr uint32_t kTab = CAP < 16384 ? CAP : 16384;  // tableSize <= min(len, maxTableSize)
     static constexpr uint32_t kDummy = kTab + 2 * kSeDcnt;
-    static constexpr uint32_t kWords = (CAP + 16) / 4 + kTab * sizeof(se_tab_t) / 4 + kSeDcnt + 32;
+    static constexpr uint32_t kBlk = GSRC ? 0u : (CAP + 16) / 4;
+    static constexpr uint32_t kWords = kBlk + kTab * sizeof(se_tab_t) / 4 + kSeDcnt + 32;
 };
 
 struct SkipTab {
@@ -76,6 +78,32 @@ __device__ __forceinline__ uint32_t ld32a(const uint32_t *in32, uint32_t p) {
 }
 // lane i's value for a wave-uniform i: v_readlane, not an LDS permute
 __device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
+
+// The block the matcher reads.  SrcLds: staged in LDS with 16 zero bytes after it (reads past
+// the end land in the zero bytes or the table: never used, the matcher clips every compare to
+// the block length).  SrcGlb: the value in global memory, read in place (L2-resident after the
+// first touch); the copy loop's window loads near the block's end (tail: positions up to
+// len + 66) clamp the address into the block instead, so nothing past the value is read.
+struct SrcLds {
+    const uint8_t *in;
+    __device__ __forceinline__ uint32_t w(uint32_t p) const { return ld32a(reinterpret_cast<const uint32_t *>(in), p); }
+    __device__ __forceinline__ uint32_t b(uint32_t p) const { return in[p]; }
+    __device__ __forceinline__ uint32_t wt(uint32_t p) const { return w(p); }
+    __device__ __forceinline__ uint32_t bt(uint32_t p) const { return b(p); }
+};
+typedef uint32_t u32_unal __attribute__((aligned(1)));
+struct SrcGlb {
+    const uint8_t *g;
+    uint32_t len;  // >= SE_MINNONLIT
+    __device__ __forceinline__ uint32_t w(uint32_t p) const { return *reinterpret_cast<const u32_unal *>(g + p); }
+    __device__ __forceinline__ uint32_t b(uint32_t p) const { return g[p]; }
+    // tail forms: in[p ..) exact for the bytes below len, anything above it
+    __device__ __forceinline__ uint32_t wt(uint32_t p) const {
+        const uint32_t q = min(p, len - 4);
+        return w(q) >> (8 * min(p - q, 3u));
+    }
+    __device__ __forceinline__ uint32_t bt(uint32_t p) const { return g[min(p, len - 1)]; }
+};
 
 struct Out {
     uint8_t *g;   // global destination of this value's stream
@@ -156,7 +184,8 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
 }
 
-__device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, uint32_t lane) {
+template <class S>
+__device__ __forceinline__ void se_flush(Out &o, const S &in, OpRing &r, uint32_t lane) {
     const bool act = lane < r.n;
     // (no lane-0 select here: the compiler turned one into an exec-masked branch around the
     // DPP, and a DPP move reading an inactive lane returns `old`)
@@ -206,7 +235,7 @@ __device__ __forceinline__ void se_flush(Out &o, const uint8_t *in, OpRing &r, u
         lm &= lm - 1;
         const uint32_t ll = lane_val(lit, k), s0 = lane_val(base, k) - ll;
         uint8_t *d0 = o.g + o.d + (lane_val(incl, k) - lane_val(sz, k)) + lane_val(lh, k);
-        for (uint32_t t = lane; t < ll; t += 64) d0[t] = in[s0 + t];
+        for (uint32_t t = lane; t < ll; t += 64) d0[t] = (uint8_t)in.b(s0 + t);
     }
     o.d += total;
     r.e0 = lane_val(r.e, r.n - 1);
@@ -281,8 +310,8 @@ hipError_t launch_lds_order_probe(hipStream_t stream, uint32_t *bad) {
 // iterations up to it.  `eq` holds in[c .. c + 4) == u for the pre-batch c; lanes whose
 // candidate changes are re-checked.  Returns the event lane (>= nl: none in this batch) and
 // m_js, whether it is a match.
-template <uint32_t DUMMY>
-__device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
+template <uint32_t DUMMY, class S>
+__device__ __forceinline__ uint32_t se_batch(const S &in, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                                              uint32_t nl, bool valid, uint64_t vmask, uint32_t pos, uint32_t u, uint32_t h,
                                              uint32_t &c, bool eq, bool &m_js, uint64_t *acc) {
     // lanes whose bucket (h mod 1024) a HIGHER lane of the batch shares: every lane writes its
@@ -323,7 +352,7 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
         nxt = wlane(nxt, above ? (uint32_t)__builtin_ctzll(above) : 64u, i);
     }
     uint64_t em = bal(eq);
-    if (bal(c != c0)) em = bal(ld32a(in32, c) == u);
+    if (bal(c != c0)) em = bal(in.w(c) == u);
     const uint64_t mb = vm & em;  // matches
     const uint64_t ev = (nl >= 64 ? ~0ull : ((1ull << nl) - 1ull)) & (~vm | mb);
     const uint32_t js = ev ? (uint32_t)__builtin_ctzll(ev) : 64u;
@@ -338,10 +367,9 @@ __device__ __forceinline__ uint32_t se_batch(const uint32_t *in32, se_tab_t *tab
 
 // encodeBlock on an LDS-staged block (len in [17, CAP]); tab zeroed by the caller.
 // f0 / f0n: this lane's skip offsets F[lane] and F[lane + 1] (the block's first batch).
-template <uint32_t DUMMY>
-__device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
+template <uint32_t DUMMY, class S>
+__device__ void se_block_lds(Out &o, const S &in, uint32_t len, se_tab_t *tab, uint32_t *dcnt, uint32_t lane,
                              uint32_t f0, uint32_t f0n, uint64_t *acc) {
-    const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
     len = uni(len);
     uint32_t shift = 24;
     for (uint32_t ts = 256; ts < 16384 && ts < len; ts *= 2) shift--;
@@ -375,9 +403,9 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             const bool valid = lane <= 32 && inl;
             const uint64_t vmask = bal(inl) & ((2ull << 32) - 1ull);
             const uint32_t pos = s + lane;
-            const bool eq = ld32a(in32, valid ? c : 0u) == u;
+            const bool eq = in.w(valid ? c : 0u) == u;
             bool m;
-            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 33, valid, vmask, pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in, tab, dcnt, lane, 33, valid, vmask, pos, u, h, c, eq, m, acc);
             if (js < 33) {
                 found = true;
                 if (!m) remainder = true;
@@ -398,12 +426,12 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // s < 64 Ki and F[k] <= 2^31 - 1: the sums fit in 32 bits
             const bool valid = s + fk1 <= sLimit;
             const uint32_t pos = valid ? s + fk : 0u;
-            const uint32_t u = ld32a(in32, pos);
+            const uint32_t u = in.w(pos);
             const uint32_t h = se_hash(u, shift) & tmask;
             uint32_t c = tab[h];  // invalid lanes hash position 0: any entry, unused
-            const bool eq = ld32a(in32, c) == u;
+            const bool eq = in.w(c) == u;
             bool m;
-            const uint32_t js = se_batch<DUMMY>(in32, tab, dcnt, lane, 64, valid, bal(valid), pos, u, h, c, eq, m, acc);
+            const uint32_t js = se_batch<DUMMY>(in, tab, dcnt, lane, 64, valid, bal(valid), pos, u, h, c, eq, m, acc);
             if (js < 64) {
                 found = true;
                 if (!m) remainder = true;
@@ -430,8 +458,9 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             // the loop's phis and kept them (and everything computed from them) in VGPRs
             s = uni(s);
             cand = uni(cand);
-            const uint32_t U = ld32a(in32, s + lane);
-            const uint32_t V = in[cand + lane];
+            const bool tail = s + 67 > len;  // (wave-uniform) the window reaches past the block
+            const uint32_t U = tail ? in.wt(s + lane) : in.w(s + lane);
+            const uint32_t V = tail ? in.bt(cand + lane) : in.b(cand + lane);
             const uint32_t hU = se_hash(U, shift) & tmask;
             const uint32_t tU = tab[hU];
             const uint64_t mm = bal((U & 0xffu) != V);
@@ -446,7 +475,9 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
             uint32_t r0 = s;  // start of the round that found the mismatch
             while (f == 64u) {
                 r0 += 64;
-                const uint64_t m2 = bal(in[r0 + lane] != in[cand + (r0 - s) + lane]);
+                const bool t2 = r0 + 64 > len;
+                const uint64_t m2 = bal(t2 ? in.bt(r0 + lane) != in.bt(cand + (r0 - s) + lane)
+                                           : in.b(r0 + lane) != in.b(cand + (r0 - s) + lane));
                 f = min(uni(m2 ? (uint32_t)__builtin_ctzll(m2) : 64u), len - r0);
             }
             const uint32_t e = r0 + f;
@@ -461,7 +492,7 @@ __device__ void se_block_lds(Out &o, const uint8_t *in, uint32_t len, se_tab_t *
                 currHash = lane_val(hU, q);
                 tc = lane_val(tU, q);
             } else {  // x = in[s - 1 .. s + 7), then Go's lookup
-                const uint32_t x0 = uni(ld32a(in32, s - 1)), x1 = uni(ld32a(in32, s + 3));
+                const uint32_t x0 = uni(in.w(s - 1)), x1 = uni(in.w(s + 3));
                 prevHash = se_hash(x0, shift) & tmask;
                 currHash = se_hash(x0 >> 8 | x1 << 24, shift) & tmask;
                 tc = uni(tab[currHash]);
@@ -633,7 +664,7 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
                     *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
                 wsync();
                 hook();
-                se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
+                se_block_lds<LY::kDummy>(o, SrcLds{in}, blen, tab, dcnt, lane, f0, f0n, acc);
             }
         }
         hook();  // (values with no LDS block)
@@ -764,20 +795,24 @@ __global__ __launch_bounds__(256) void k_enc_bemit(const uint64_t *__restrict__ 
     }
 }
 
-// one wave per 64-KiB block (one per CU: block + 16-K-entry table ~ 98 KiB of LDS), blocks taken
-// from a queue: encodeBlock (or emitLiteral for a last block under 17 bytes) into the block's slot,
-// its length into bclen
+// one wave per 64-KiB block, blocks taken from a queue: encodeBlock (or emitLiteral for a last
+// block under 17 bytes) into the block's slot, its length into bclen.  The matcher reads the block
+// in place (SrcGlb): LDS holds only the 16-K-entry table (33 KiB), so 4 waves run per CU.  With
+// the block staged in LDS too (98 KiB, one wave per CU) bench.py --config bigval encoded at 20.5
+// GiB/s against 40.4 (profiles/r6/bigval/enc_blocks_gsrc.txt); for the <= 4 KiB values the
+// staged block wins (C4 179 vs 145 GiB/s with the value read in place, profiles/r6/c4_gsrc/):
+// their limit is one wave's latency chain, not the waves per CU.
+constexpr uint32_t kSeBlockWaves = 4;
 __global__ __launch_bounds__(64) void k_snappy_enc_blocks(const uint8_t *__restrict__ vals,
                                                           const uint64_t *__restrict__ val_off,
                                                           const uint64_t *__restrict__ bbase, uint32_t n,
                                                           const uint2 *__restrict__ ent, uint32_t *__restrict__ head,
                                                           uint8_t *__restrict__ bscr, const uint64_t *__restrict__ bsoff,
                                                           uint32_t *__restrict__ bclen) {
-    typedef SeLayout<SE_CAP_BLOCK> LY;
+    typedef SeLayout<SE_CAP_BLOCK, true> LY;
     __shared__ __attribute__((aligned(16))) uint32_t lds[LY::kWords];
-    uint8_t *in = reinterpret_cast<uint8_t *>(lds);
-    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + (SE_CAP_BLOCK + 16) / 4);
-    uint32_t *dcnt = lds + (SE_CAP_BLOCK + 16) / 4 + LY::kTab * sizeof(se_tab_t) / 4;
+    se_tab_t *tab = reinterpret_cast<se_tab_t *>(lds + LY::kBlk);
+    uint32_t *dcnt = lds + LY::kBlk + LY::kTab * sizeof(se_tab_t) / 4;
     const uint32_t lane = threadIdx.x;
     for (uint32_t j = lane; j < kSeDcnt; j += 64) dcnt[j] = 0;
     const uint32_t f0 = kSkip.f[lane], f0n = kSkip.f[lane + 1];
@@ -799,28 +834,15 @@ __global__ __launch_bounds__(64) void k_snappy_enc_blocks(const uint8_t *__restr
         if (blen < SE_MINNONLIT) {
             se_emit_literal(o, nullptr, bs, blen, lane);
         } else {
-            for (uint32_t t = 16 * lane; t < blen; t += 1024) {
-                u32x4 v;
-                if (t + 16 <= blen) {
-                    v = gld<u32x4u>((uint64_t)(bs + t));
-                } else {
-                    uint32_t w[4] = {0, 0, 0, 0};
-                    for (uint32_t b = 0; t + b < blen; b++) w[b >> 2] |= (uint32_t)bs[t + b] << (8 * (b & 3));
-                    v = u32x4{w[0], w[1], w[2], w[3]};
-                }
-                *reinterpret_cast<u32x4 *>(in + t) = v;
-            }
-            wsync();
-            for (uint32_t t = blen + lane; t < blen + 16; t += 64) in[t] = 0;
             uint32_t ts = 256;
             while (ts < 16384 && ts < blen) ts *= 2;
             for (uint32_t t = 8 * lane; t < ts; t += 512) *reinterpret_cast<u32x4 *>(tab + t) = u32x4{0, 0, 0, 0};
             wsync();
-            se_block_lds<LY::kDummy>(o, in, blen, tab, dcnt, lane, f0, f0n, acc);
+            se_block_lds<LY::kDummy>(o, SrcGlb{bs, blen}, blen, tab, dcnt, lane, f0, f0n, acc);
         }
         if (lane == 0) bclen[q] = o.d;
         q = uni(nq);
-        wsync();  // the next block's staging overwrites the LDS the matcher read
+        wsync();  // the next block's table reset overwrites the LDS the matcher read
     }
 }
 
@@ -911,8 +933,8 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
     if (hipError_t e = launch_exclusive_scan_u64(L, bbase, bbase, n, scan)) return e;
     if (hipError_t e = launch_exclusive_scan_u64(L, bsoff, bsoff, n, scan)) return e;
     hipLaunchKernelGGL(k_enc_bemit, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, bbase, n, ent);
-    hipLaunchKernelGGL(k_snappy_enc_blocks, dim3(L.num_cus), dim3(64), 0, L.stream, vals, val_off, bbase, n, ent, bhead,
-                       bscr, bsoff, bclen);
+    hipLaunchKernelGGL(k_snappy_enc_blocks, dim3(L.num_cus * kSeBlockWaves), dim3(64), 0, L.stream, vals, val_off, bbase,
+                       n, ent, bhead, bscr, bsoff, bclen);
     hipLaunchKernelGGL(k_snappy_concat, dim3(lane_grid(L, (uint64_t)n * 64, 256)), dim3(256), 0, L.stream, val_off, n,
                        bbase, bscr, bsoff, bclen, scratch, scap, soff, clen);
     return hipGetLastError();

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 6 GPU calls: TESTS (pytest files), SMOKE=1, AB=<n> (C2 --warmup 5 vs 100, with and without
-# the clock ramp, n alternations), BENCH="<args>" (one extra bench line), PROF="<bench args>" (rocprof stats)
+# the clock ramp, n alternations), BENCH="<args>" (one extra bench line), PROF="<bench args>" (rocprof stats),
+# ABENV=<var> ABARGS="<bench args>" ABN=<n>: the bench line with <var>=0 and =1, n alternations
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -33,6 +34,15 @@ if [ -n "$BENCH" ]; then
     timeout -k 10 400 python3 -u bench.py $args > $f 2> $f.err || { tail -20 $f.err; exit 1; }
     echo "bench $i ($args): $(tail -c 600 $f)"
   done <<< "$BENCH"
+fi
+if [ -n "$ABENV" ]; then
+  for r in $(seq 1 ${ABN:-3}); do
+    for v in 0 1; do
+      f=$O/abenv_${v}_$r.json
+      env $ABENV=$v timeout -k 10 300 python3 -u bench.py $ABARGS > $f 2> $f.err || { tail -20 $f.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$f')); print('$ABENV=$v run $r', d['value'], d['ms_per_step'])"
+    done
+  done
 fi
 if [ -n "$PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py $PROF > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
