@@ -414,10 +414,13 @@ int bhg_decode_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     Scratch sc;
     const size_t scan_b = (bhg::scan_scratch_bytes(n) + 255) & ~(size_t)255;
     const size_t list_b = out_vals ? (bhg::snappy_list_bytes(n) + 255) & ~(size_t)255 : 0;
-    const size_t big_b = out_vals ? bhg::snappy_big_bytes(n, out_vals_cap) : 0;
-    if (int r = scratch_alloc(c, L.stream, scan_b + list_b + big_b, sc)) return r;
+    const size_t big_b = out_vals ? (bhg::snappy_big_bytes(n, out_vals_cap) + 255) & ~(size_t)255 : 0;
+    // long records: their CRCs by the long-record pass after the header pass (bhg_longcrc.hip)
+    const size_t long_b = bhg::long_batch(src_len, n) ? bhg::long_crc_scratch_bytes(n, src_len) : 0;
+    if (int r = scratch_alloc(c, L.stream, scan_b + list_b + big_b + long_b, sc)) return r;
     uint32_t *lists = out_vals ? reinterpret_cast<uint32_t *>(sc.base + scan_b) : nullptr;
-    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off, lists));
+    HIP_TRY(c, bhg::launch_decode(L, src, src_len, handles, n, codec, expected_crc, out_desc, out_val_off, lists,
+                                  long_b ? sc.base + scan_b + list_b + big_b : nullptr));
     HIP_TRY(c, bhg::launch_exclusive_scan_u64(L, out_val_off, out_val_off, n, sc.base));
     if (out_vals)
         HIP_TRY(c, bhg::launch_snappy(L, src, src_len, handles, n, out_desc, out_vals, out_vals_cap, out_val_off, lists,

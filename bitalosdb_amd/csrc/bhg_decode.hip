@@ -197,11 +197,12 @@ size_t crc_long_scratch_bytes(uint32_t n) { return (size_t)n * kLongParts * 4; }
 // host launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes, uint32_t *lists) {
+                         int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes, uint32_t *lists,
+                         void *long_scratch) {
     if (codec == BHG_CODEC_NONE) return launch_decode_tile(L, src, src_len, h, n, expected_crc, out);
     if (lists)  // the list sizes (the header pass appends, launch_snappy reads)
         if (hipError_t e = hipMemsetAsync(lists, 0, 4 * kSnapListHdr, L.stream)) return e;
-    return launch_decode_stream(L, src, src_len, h, n, 1, expected_crc, out, sizes, lists);
+    return launch_decode_stream(L, src, src_len, h, n, 1, expected_crc, out, sizes, lists, long_scratch);
 }
 
 hipError_t launch_crc_ranges(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,

@@ -82,7 +82,9 @@ __device__ __forceinline__ uint32_t ld32_clamp(uint64_t a, uint64_t lo4, uint64_
 // KO (lab only, knock-outs for timing; outputs are then wrong): bit 0 no CRC
 // chains, 1 no scan, 2 no header loads, 3 no chain fold, 4 uniform-m locate,
 // 5 no head init / tail, 6 no descriptor stores, 7 no shift-table loads in the prologue.
-template <int MODE, int NCH, int WPB, int WIN = 128, int PIPE = 0, int KO = 0>
+// LONG: records longer than kLongRec own no windows (the header words are loaded on their own); their
+// CRC and CRC status are left to the long-record pass (launch_long_crc), run right after this one
+template <int MODE, int NCH, int WPB, int WIN = 128, int PIPE = 0, int KO = 0, int LONG = 0>
 __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__restrict__ src, uint64_t src_len,
                                                             const bhg_handle *__restrict__ handles, uint32_t n,
                                                             const uint32_t *__restrict__ expected_crc,
@@ -153,7 +155,8 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
         }
         const uint32_t L = inb ? h.length : 0u;
         const uint64_t p = base + (inb ? h.offset : 0ull);
-        const uint32_t m = (uint32_t)(((uint64_t)L + WIN - 1) / WIN);
+        const bool lrec = LONG && L > kLongRec;
+        const uint32_t m = lrec ? 0u : (uint32_t)(((uint64_t)L + WIN - 1) / WIN);
         const uint32_t pad = (uint32_t)WIN * m - L;  // 0..WIN-1 (head left padding)
         const uint32_t ecrc = ecp[(i < n ? i : n - 1) & emask];
         // record-major window numbering: M = exclusive prefix of m over the tile
@@ -391,6 +394,10 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
             if (interior) run(true);
             else run(false);
         }
+        if (LONG && lrec) {
+#pragma unroll
+            for (int t = 0; t < 16; t++) hw[t] = ld32_clamp((p & ~3ull) + 4 * t, lo4, hi4);
+        }
         wait_loads_done();  // unconditional: see bhg_device.h
         if (KO & 1024) {  // lab: no record section
             if (rcrc == 0x9e3779b9u) out[i].crc = rcrc;
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                 for (int u = 0; u < 15; u++) rw[u] = __builtin_amdgcn_alignbyte(hw[u + 1], hw[u], hsh);
                 const uint32_t k = L >= 12 ? rw[0] : 0u, v = L >= 12 ? rw[1] : 0u, fn = L >= 12 ? rw[2] : 0u;
                 const bool rvalid = L >= 12 && k != 0 && v != 0 && (uint64_t)12 + k + v == (uint64_t)L;  // block2.go:57-66
-                dcrc = crc_mask(~rcrc);                                                                    // crc.go:31-33
+                dcrc = lrec ? 0u : crc_mask(~rcrc);                                                        // crc.go:31-33
                 if (rvalid) {
                     uint32_t key_len = 0, fnv = BHG_FNV_OFFSET;
                     uint64_t trailer = 255;  // InternalKeyKindInvalid when ikeySize < 8
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(64 * WPB) void k_decode_stream(const uint8_t *__res
                             vlen = v;
                         }
                     }
-                    if (expected_crc != nullptr && dst == BHG_ST_OK && ecrc != dcrc) dst = BHG_ST_CRC_MISMATCH;
+                    if (expected_crc != nullptr && dst == BHG_ST_OK && ecrc != dcrc && !lrec) dst = BHG_ST_CRC_MISMATCH;
                 } else {
                     dst = BHG_ST_RECORD_NIL;  // ErrBhReadRecordNil (reader.go:260-264)
                 }

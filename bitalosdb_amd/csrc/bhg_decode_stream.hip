@@ -16,17 +16,26 @@ void build_stream_tab_default(uint32_t *out) { build_stream_tab(out, kStreamWin,
 // slower, DESIGN.md 4.1, and stays a lab build)
 hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                                 int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
-                                uint32_t *lists) {
+                                uint32_t *lists, void *long_scratch) {
     if (mode != 1) return hipErrorInvalidValue;
     constexpr int WPB = 8;  // 156.5 KiB of LDS: one workgroup per CU
     const uint64_t tiles = (n + 63) / 64;
     const uint64_t need = (tiles + WPB - 1) / WPB, cap = (uint64_t)L.num_cus;
     uint32_t grid = (uint32_t)(need < cap ? need : cap);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_decode_stream<1, kStreamNch, WPB, kStreamWin, kStreamPipe>), dim3(grid),
+    if (!long_scratch) {
+        hipLaunchKernelGGL((k_decode_stream<1, kStreamNch, WPB, kStreamWin, kStreamPipe>), dim3(grid),
+                           dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab, lists,
+                           (uint32_t)snappy_sub_cap(n));
+        return hipGetLastError();
+    }
+    // a batch of long records (long_batch): one wave streaming a multi-MiB record's windows was the
+    // step's tail (bench.py --config bigval: 2.2 ms); their CRCs go to the whole-chip pass instead
+    hipLaunchKernelGGL((k_decode_stream<1, kStreamNch, WPB, kStreamWin, kStreamPipe, 0, 1>), dim3(grid),
                        dim3(64 * WPB), 0, L.stream, src, src_len, h, n, expected_crc, out, sizes, L.stab, lists,
                        (uint32_t)snappy_sub_cap(n));
-    return hipGetLastError();
+    if (hipError_t e = hipGetLastError()) return e;
+    return launch_long_crc(L, src, src_len, h, n, expected_crc, out, long_scratch);
 }
 
 }  // namespace bhg

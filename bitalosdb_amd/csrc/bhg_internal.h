@@ -49,9 +49,11 @@ inline uint32_t resident_per_cu(const void *kernel, int block, uint32_t fallback
 // pass (sizes[i] = decoded length; the values follow with launch_snappy)
 // lists: null, or (snappy) the decode lists of snappy_list_bytes(n) -- the header pass sorts the
 // blocks to decode into them by size for launch_snappy (which must get the same pointer)
+// long_scratch (snappy): null, or long_crc_scratch_bytes(n, src_len) -- then the records longer than
+// kLongRec are CRC'd by the long-record pass after the header pass (a batch of long records: long_batch)
 hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                          int codec, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
-                         uint32_t *lists = nullptr);
+                         uint32_t *lists = nullptr, void *long_scratch = nullptr);
 // bhg_decode_tile.hip: the NoCompressor decode kernel.  long_scratch: null, or long_crc_scratch_bytes(n,
 // src_len) bytes -- then records longer than kLongRec are CRC'd by the long-record pass (a batch of long
 // records: see long_batch)
@@ -73,7 +75,7 @@ size_t stream_tab_words();
 void build_stream_tab_default(uint32_t *out);
 hipError_t launch_decode_stream(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                                 int mode, const uint32_t *expected_crc, bhg_desc *out, uint64_t *sizes,
-                                uint32_t *lists);
+                                uint32_t *lists, void *long_scratch = nullptr);
 // bhg_snappy_dec.hip: golang/snappy value decode (lane per block)
 // list: the decode lists the header pass filled (launch_decode with the same pointer, of
 // snappy_list_bytes(n)): the blocks for the 1-KiB LDS slots, those for the 4-KiB slots in

@@ -746,65 +746,174 @@ __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restri
 //   k_snappy_rt the serial pass over that list (exact golang/snappy statuses).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSbChunk = 65536;  // decoded bytes per chunk (at least: a chunk starts at an element)
+constexpr uint32_t kSbSeg = 16384;    // stream bytes per segment of a long stream's parse
+constexpr uint32_t kSbSegMin = 2 * kSbSeg;  // streams longer than this: the segment parse
+constexpr uint32_t kSbBad = 0x10000u; // a window exit: the chain met an irregular element
 struct SbEnt {
     uint32_t i, s0, d0, last;  // block, stream start (after the uvarint header), output start; ~0 = unused slot
 };
-// layout of the big path's scratch: [0] chunk entries reserved, [1] serial list size; from 256 B the
-// entries (cap), the per-block words {chunks left, failed} (n), the serial list (n)
+struct SbBig {
+    uint32_t i, seg0, nseg, b0;  // block, its first segment, segments, first chunk slot
+};
+// layout of the big path's scratch: [0] chunk slots reserved, [1] serial list size, [2] segments
+// reserved, [3] segment-parsed blocks; from 256 B the chunk entries (cap), the per-block words
+// {chunks left, failed} (n), the serial list (n), the segment-parsed blocks (n), then per segment
+// (segcap) its block's index in that list, its entry (stream position, output), and the 64 chain
+// results of the speculative parse
 static size_t al256_(size_t x) { return (x + 255) & ~(size_t)255; }
 static uint64_t sb_cap(uint32_t n, uint64_t out_cap) { return out_cap / kSbChunk + n + 1; }
+static uint64_t sb_segcap(uint32_t n, uint64_t out_cap) { return out_cap / kSbSeg + n + 1; }
+constexpr uint32_t kSbMark = 1024;              // checkpoint spacing of chain 0 in a segment
+constexpr uint32_t kSbMarks = kSbSeg / kSbMark; // checkpoints per segment (index 0 unused)
 size_t snappy_big_bytes(uint32_t n, uint64_t out_cap) {
-    return 256 + al256_(sb_cap(n, out_cap) * sizeof(SbEnt)) + al256_((size_t)n * 8) + al256_((size_t)n * 4);
+    const uint64_t sc = sb_segcap(n, out_cap);
+    return 256 + al256_(sb_cap(n, out_cap) * sizeof(SbEnt)) + al256_((size_t)n * 8) + al256_((size_t)n * 4) +
+           al256_((size_t)n * sizeof(SbBig)) + al256_(sc * 4) + al256_(sc * 8) + al256_(sc * 64 * 8) +
+           al256_(sc * kSbMarks * 8);
 }
 struct SbScratch {
     uint32_t *ctr;
     SbEnt *ent;
     uint32_t *blk, *ser;
-    uint64_t cap;
+    SbBig *bigs;
+    uint32_t *segblk;
+    uint2 *segent, *res, *ck;
+    uint64_t cap, segcap;
 };
 static SbScratch sb_layout(void *p, uint32_t n, uint64_t out_cap) {
     SbScratch S;
     uint8_t *b = static_cast<uint8_t *>(p);
     S.ctr = reinterpret_cast<uint32_t *>(b);
     S.cap = sb_cap(n, out_cap);
-    S.ent = reinterpret_cast<SbEnt *>(b + 256);
-    S.blk = reinterpret_cast<uint32_t *>(b + 256 + al256_(S.cap * sizeof(SbEnt)));
-    S.ser = S.blk + al256_((size_t)n * 8) / 4;
+    S.segcap = sb_segcap(n, out_cap);
+    b += 256;
+    S.ent = reinterpret_cast<SbEnt *>(b);
+    b += al256_(S.cap * sizeof(SbEnt));
+    S.blk = reinterpret_cast<uint32_t *>(b);
+    b += al256_((size_t)n * 8);
+    S.ser = reinterpret_cast<uint32_t *>(b);
+    b += al256_((size_t)n * 4);
+    S.bigs = reinterpret_cast<SbBig *>(b);
+    b += al256_((size_t)n * sizeof(SbBig));
+    S.segblk = reinterpret_cast<uint32_t *>(b);
+    b += al256_(S.segcap * 4);
+    S.segent = reinterpret_cast<uint2 *>(b);
+    b += al256_(S.segcap * 8);
+    S.res = reinterpret_cast<uint2 *>(b);
+    b += al256_(S.segcap * 64 * 8);
+    S.ck = reinterpret_cast<uint2 *>(b);
     return S;
 }
 
 constexpr uint32_t kSbBuf = 4096;  // staged stream bytes per wave (+ 128 of look-ahead)
+constexpr uint32_t kSbLanes = 8;   // chunks per wave in k_sb_walk
+
+// a listed block's stream: S (absolute, after the uvarint header), slen, dlen
+struct SbStream {
+    uint64_t S;
+    uint32_t slen, dlen;
+};
+__device__ __forceinline__ SbStream sb_stream(uint64_t base, const bhg_handle *handles, const bhg_desc *out, uint32_t i) {
+    const uint32_t *dw = reinterpret_cast<const uint32_t *>(out + i);
+    const bhg_handle hh = handles[i];
+    const uint64_t cp = base + hh.offset + dw[2];
+    uint32_t hdr = 0;
+    while (hdr < 10 && gld<uint8_t>(cp + hdr) >= 0x80) hdr++;  // uvarint decodedLen (validated by the header pass)
+    hdr++;
+    return SbStream{cp + hdr, hh.length - dw[2] - hdr, dw[3]};
+}
+
+// [bb, bb + kSbBuf + 128) of the stream into buf (bytes past the stream: 0)
+__device__ __forceinline__ void sb_stage(uint8_t *buf, const SbStream &T, uint32_t bb, uint32_t lane) {
+    sl_wsync();
+    for (uint32_t t = 16 * lane; t < kSbBuf + 128; t += 1024) {
+        u32x4 v = {0, 0, 0, 0};
+        if ((uint64_t)bb + t + 16 <= T.slen) v = gld<u32x4u>(T.S + bb + t);
+        else if (bb + t < T.slen) v = ld16_hi(T.S + bb + t, T.S + T.slen);
+        *reinterpret_cast<u32x4_lds_u *>(buf + t) = v;
+    }
+    sl_wsync();
+}
+
+// One window of the tag-only parse: the positions e .. e + lim - 1 (lim <= 64; buf holds the
+// stream from bb).  Lane q: the element a tag at e + q would be (elen: its stream length, 0 when
+// its length bytes or data pass the stream, or a literal is longer than dlen or 2^26 -- never
+// golang/snappy's, whose blocks are 64 KiB -- so that a window's output sum cannot wrap; olen: its
+// output length), then by pointer doubling (ds_bpermute) nx = the position (relative to e) after
+// the elements from e + q up to the first one at or past lim, kSbBad or more when one of them is
+// irregular, and sm = their output.  6 levels cover the <= 32 elements of 64 bytes.
+struct SbWin {
+    uint32_t elen, olen, nx, sm;
+};
+__device__ __forceinline__ SbWin sb_window(const uint8_t *buf, uint32_t bb, uint32_t e, uint32_t lim, uint32_t slen,
+                                           uint32_t dlen, uint32_t lane) {
+    const uint32_t p = e + lane, x = p - bb;
+    uint32_t elen = 0, olen = 0;
+    if (p < slen) {
+        const uint32_t tag = buf[x], ty = tag & 3u, v = tag >> 2;
+        if (ty == 0) {
+            uint32_t ln = v + 1, nb = 0;
+            if (v >= 60) {
+                nb = v - 59;
+                uint32_t lv = 0;
+                for (uint32_t q = 0; q < 4; q++) lv |= q < nb ? (uint32_t)buf[x + 1 + q] << (8 * q) : 0u;
+                ln = lv + 1;  // 0 for a 4-byte 2^32 - 1: irregular
+            }
+            const uint64_t el = 1ull + nb + ln;
+            if (p + 1 + nb <= slen && ln != 0 && ln <= dlen && ln <= (1u << 26) && p + el <= slen) {
+                elen = (uint32_t)el;
+                olen = ln;
+            }
+        } else {
+            const uint32_t el = ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+            if (p + el <= slen) { elen = el; olen = ty == 1 ? 4 + (v & 7) : 1 + v; }
+        }
+    }
+    uint32_t nx = elen ? lane + elen : kSbBad, sm = olen;
+#pragma unroll
+    for (int lv = 0; lv < 6; lv++) {
+        const bool in = nx < lim;
+        const int a = (int)((in ? nx : 0u) * 4u);
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)nx);
+        const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)sm);
+        if (in) { nx = nn; sm += ns; }
+    }
+    return SbWin{elen, olen, nx, sm};
+}
+
+// Blocks past the LDS tiers, one WAVE per listed block.  A block of <= 64 KiB decoded is one chunk
+// without a parse.  A stream of <= kSbSegMin bytes is parsed here, window by window (the chain from
+// the block start; at a window that holds a 64-KiB output boundary its elements one by one, with
+// v_readlane), cutting the block at the first element at or past every 64 KiB of output.  Longer
+// streams are handed to the segment parse (k_sb_seg -> k_sb_stitch -> k_sb_emit): the round-6
+// bigval batch's 4-MiB values took 14.7 ms here, one window after another.  Anything irregular (a
+// length past the stream, output past dlen, not ending exactly at the stream end) sends the block
+// to the serial pass.
 __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ src, uint64_t src_len,
                                                   const bhg_handle *__restrict__ handles, uint32_t n,
                                                   bhg_desc *__restrict__ out, uint64_t out_cap,
                                                   const uint64_t *__restrict__ val_off,
                                                   const uint32_t *__restrict__ rt_cnt, const uint32_t *__restrict__ rt_ent,
                                                   uint32_t *__restrict__ ctr, SbEnt *__restrict__ ent, uint64_t cap,
-                                                  uint32_t *__restrict__ blk, uint32_t *__restrict__ ser) {
+                                                  uint32_t *__restrict__ blk, uint32_t *__restrict__ ser,
+                                                  SbBig *__restrict__ bigs, uint32_t *__restrict__ segblk, uint64_t segcap) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[4][kSbBuf + 128];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint8_t *buf = bufs[w];
-    const uint64_t base = (uint64_t)src, end = base + src_len;
+    const uint64_t base = (uint64_t)src;
     const uint32_t cnt = *rt_cnt;
     for (uint32_t j = blockIdx.x * 4 + w; j < cnt; j += gridDim.x * 4) {
         const uint32_t i = rt_ent[j];
         uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
         const uint32_t status = dw[9];
         if (status != BHG_ST_OK && status != BHG_ST_CRC_MISMATCH) continue;
-        const uint32_t cpos = dw[2], dlen = dw[3];
+        const uint32_t dlen = dw[3];
         const uint64_t o0 = val_off[i], o1 = val_off[i + 1];
         if (o1 > out_cap || o1 - o0 < dlen) {  // as k_snappy_rt
             if (lane == 0) { dw[2] = 0; dw[3] = 0; dw[9] = BHG_ST_SNAPPY_TOO_LARGE; }
             continue;
         }
-        const bhg_handle hh = handles[i];
-        const uint64_t cp = base + hh.offset + cpos;
-        const uint32_t clen = hh.length - cpos;
-        uint32_t hdr = 0;
-        while (hdr < 10 && gld<uint8_t>(cp + hdr) >= 0x80) hdr++;  // uvarint decodedLen (validated by the header pass)
-        hdr++;
-        const uint64_t S = cp + hdr;
-        const uint32_t slen = clen - hdr;
+        const SbStream T = sb_stream(base, handles, out, i);
         // chunk slots: at most one per 64 KiB of output, plus the first
         const uint32_t k = dlen / kSbChunk + 1;
         uint32_t b0 = 0;
@@ -815,63 +924,33 @@ __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ sr
             for (uint32_t q = lane; (uint64_t)b0 + q < cap && q < k; q += 64) ent[b0 + q] = SbEnt{~0u, 0, 0, 0};
             continue;
         }
+        if (dlen > kSbChunk && T.slen > kSbSegMin) {  // the segment parse, when its scratch holds the segments
+            const uint32_t nseg = (T.slen + kSbSeg - 1) / kSbSeg;
+            uint32_t s0 = 0;
+            if (lane == 0) s0 = atomicAdd(ctr + 2, nseg);
+            s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
+            if ((uint64_t)s0 + nseg <= segcap) {
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(ctr + 3, 1u);  // < n: one entry per listed block at most
+                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+                if (lane == 0) bigs[t] = SbBig{i, s0, nseg, b0};
+                for (uint32_t q = lane; q < nseg; q += 64) segblk[s0 + q] = t;
+                continue;
+            }
+            // (the one reservation that crosses segcap: its segments below it are marked unused)
+            for (uint64_t q = (uint64_t)s0 + lane; q < segcap; q += 64) segblk[q] = ~0u;
+        }
         uint32_t ci = 1;
         bool bad = false;
         if (dlen > kSbChunk) {
             uint32_t e = 0, d = 0, nextb = kSbChunk, bb = ~0u;
-            while (e < slen) {
-                if (bb == ~0u || e + 64 + 8 > bb + kSbBuf) {  // restage [e, e + kSbBuf + 128) (bytes past the stream: 0)
-                    bb = e;
-                    sl_wsync();
-                    for (uint32_t t = 16 * lane; t < kSbBuf + 128; t += 1024) {
-                        u32x4 v = {0, 0, 0, 0};
-                        if ((uint64_t)bb + t + 16 <= slen) v = gld<u32x4u>(S + bb + t);
-                        else if (bb + t < slen) v = ld16_hi(S + bb + t, S + slen);
-                        *reinterpret_cast<u32x4_lds_u *>(buf + t) = v;
-                    }
-                    sl_wsync();
-                }
-                // lane: the element a tag at e + lane would be (elen 0: its length bytes pass the stream)
-                const uint32_t p = e + lane, x = p - bb;
-                uint32_t elen = 0, olen = 0;
-                if (p < slen) {
-                    const uint32_t tag = buf[x], ty = tag & 3u, v = tag >> 2;
-                    if (ty == 0) {
-                        uint32_t ln = v + 1, nb = 0;
-                        if (v >= 60) {
-                            nb = v - 59;
-                            uint32_t lv = 0;
-                            for (uint32_t q = 0; q < 4; q++) lv |= q < nb ? (uint32_t)buf[x + 1 + q] << (8 * q) : 0u;
-                            ln = lv + 1;  // 0 for a 4-byte 2^32 - 1: caught as irregular (ln > dlen)
-                        }
-                        const uint64_t el = 1ull + nb + ln;
-                        // (a literal past 64 MiB -- never golang/snappy's, its blocks are 64 KiB -- is left
-                        // to the serial pass, so that a window's output sum cannot wrap)
-                        if (p + 1 + nb <= slen && ln != 0 && ln <= dlen && ln <= (1u << 26) && p + el <= slen) {
-                            elen = (uint32_t)el;
-                            olen = ln;
-                        }
-                    } else {
-                        const uint32_t el = ty == 1 ? 2u : ty == 2 ? 3u : 5u;
-                        if (p + el <= slen) { elen = el; olen = ty == 1 ? 4 + (v & 7) : 1 + v; }
-                    }
-                }
-                // the chain from e through the window by pointer doubling (ds_bpermute): lane b ends at
-                // nx = the position after 2^k elements from e + b (saturating at the first one past the
-                // window), sm = their output; 5 levels cover the <= 32 elements of 64 bytes (an element is
-                // >= 2 bytes).  Positions past the stream are fixed points; 0x10000: an irregular element.
-                uint32_t nx = p >= slen ? lane : (elen ? lane + elen : 0x10000u), sm = olen;
-#pragma unroll
-                for (int lv = 0; lv < 6; lv++) {
-                    const bool in = nx < 64;
-                    const int a = (int)((in ? nx : 0u) * 4u);
-                    const uint32_t nn = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)nx);
-                    const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)sm);
-                    if (in) { nx = nn; sm += ns; }
-                }
-                const uint32_t wx = (uint32_t)__builtin_amdgcn_readfirstlane((int)nx);
-                const uint32_t ws = (uint32_t)__builtin_amdgcn_readfirstlane((int)sm);
-                if (wx >= 0x10000u || ws > dlen - d) { bad = true; break; }
+            while (e < T.slen) {
+                if (bb == ~0u || e + 64 + 8 > bb + kSbBuf) sb_stage(buf, T, bb = e, lane);
+                const uint32_t lim = min(64u, T.slen - e);
+                const SbWin W = sb_window(buf, bb, e, lim, T.slen, dlen, lane);
+                const uint32_t wx = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.nx);
+                const uint32_t ws = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.sm);
+                if (wx >= kSbBad || ws > dlen - d) { bad = true; break; }
                 if (d + ws < nextb) {  // no chunk boundary in this window (the common case)
                     d += ws;
                     e += wx;
@@ -879,9 +958,9 @@ __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ sr
                 }
                 // a chunk boundary: the window's elements one by one
                 uint32_t q = 0;
-                while (q < 64 && e + q < slen) {
-                    const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)elen, (int)q);
-                    const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)olen, (int)q);
+                while (q < lim) {
+                    const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)W.elen, (int)q);
+                    const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)W.olen, (int)q);
                     if (el == 0 || ol > dlen - d) { bad = true; break; }
                     if (d >= nextb) {
                         if (lane == 0) ent[b0 + ci] = SbEnt{i, e + q, d, 0};
@@ -894,7 +973,7 @@ __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ sr
                 if (bad) break;
                 e += q;
             }
-            if (!bad && (e != slen || d != dlen)) bad = true;
+            if (!bad && (e != T.slen || d != dlen)) bad = true;
         }
         if (bad) {
             for (uint32_t q = lane; q < k; q += 64) ent[b0 + q] = SbEnt{~0u, 0, 0, 0};
@@ -911,15 +990,199 @@ __global__ __launch_bounds__(256) void k_sb_parse(const uint8_t *__restrict__ sr
     }
 }
 
+// The segment parse of a long stream, in three launches.
+//   k_sb_seg     one WAVE per segment (kSbSeg stream bytes at X0): 64 chains at once, from X0 + b for
+//                every lane b, each to the first element at or past the segment's end -- where it
+//                ends and its output (or that it met an irregular element).  Every window (at the
+//                lowest chain still in the segment) is one sb_window, each chain in it then one
+//                ds_bpermute.  The chains merge within a few elements.
+//   k_sb_stitch  one WAVE per block, its segments in order: the block's chain enters segment k at
+//                position P; the chain from X0 + (P - X0) is the block's, and ends where the next
+//                one starts.  When P >= X0 + 64 (a literal longer than 64 bytes over X0) the wave
+//                walks the segment from P itself.  Then the totals are checked as in k_sb_parse.
+//   k_sb_emit    one WAVE per segment, the block's chain through it from its entry, writing chunk
+//                slot m at the element after the one that reaches m * 64 KiB of output: the first
+//                element at or past that output.
+// (golang/snappy's stream is a sequence of 64-KiB blocks, so every chunk decodes on its own.)
+__global__ __launch_bounds__(256) void k_sb_seg(const uint8_t *__restrict__ src, const bhg_handle *__restrict__ handles,
+                                                const bhg_desc *__restrict__ out, const uint32_t *__restrict__ ctr,
+                                                const SbBig *__restrict__ bigs, const uint32_t *__restrict__ segblk,
+                                                uint64_t segcap, uint2 *__restrict__ res, uint2 *__restrict__ ck) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[4][kSbBuf + 128];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t *buf = bufs[w];
+    const uint64_t total = ctr[2] < segcap ? ctr[2] : segcap;
+    for (uint64_t j = (uint64_t)blockIdx.x * 4 + w; j < total; j += (uint64_t)gridDim.x * 4) {
+        const uint32_t sb = segblk[j];
+        if (sb == ~0u) continue;  // reserved by a block that did not fit
+        const SbBig B = bigs[sb];
+        const SbStream T = sb_stream((uint64_t)src, handles, out, B.i);
+        const uint32_t k = (uint32_t)(j - B.seg0), x0 = k * kSbSeg, x1 = min(x0 + kSbSeg, T.slen);
+        uint32_t P = x0 + lane, O = 0, bb = ~0u, cn = 1;  // cn: chain 0's next checkpoint (lane 0)
+        bool act = P < x1;
+        uint2 *const ckj = ck + j * kSbMarks;
+        for (;;) {
+            const uint32_t key = act ? P : ~0u;
+            const uint32_t E = ~(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(~key), 63);  // the lowest chain
+            if (E == ~0u) break;
+            if (bb == ~0u || E + 64 + 8 > bb + kSbBuf) sb_stage(buf, T, bb = E, lane);
+            // windows end at the checkpoint marks x0 + c kSbMark too (k_sb_stitch walks the same way)
+            const uint32_t lim = min(min(64u, x1 - E), x0 + ((E - x0) / kSbMark + 1) * kSbMark - E);
+            const SbWin W = sb_window(buf, bb, E, lim, T.slen, T.dlen, lane);
+            const uint32_t q = P - E;
+            const bool mv = act && q < lim;
+            const int a = (int)((mv ? q : 0u) * 4u);
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)W.nx);
+            const uint32_t sm = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)W.sm);
+            if (mv) {
+                if (nx >= kSbBad) {
+                    P = ~0u;
+                    act = false;
+                } else {
+                    P = E + nx;
+                    O += sm;
+                    act = P < x1;
+                    // chain 0 at every mark it reaches: its first element at or past the mark
+                    for (; lane == 0 && cn < kSbMarks && P >= x0 + cn * kSbMark; cn++) ckj[cn] = uint2{P, O};
+                }
+            }
+        }
+        for (; lane == 0 && cn < kSbMarks; cn++) ckj[cn] = uint2{~0u, 0};
+        res[j * 64 + lane] = uint2{P, O};  // P = ~0: an irregular element on the chain from x0 + lane
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sb_stitch(const uint8_t *__restrict__ src, const bhg_handle *__restrict__ handles,
+                                                   const bhg_desc *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                   SbEnt *__restrict__ ent, uint32_t *__restrict__ blk,
+                                                   uint32_t *__restrict__ ser, const SbBig *__restrict__ bigs,
+                                                   uint64_t segcap, uint2 *__restrict__ segent,
+                                                   const uint2 *__restrict__ res, const uint2 *__restrict__ ck) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[4][kSbBuf + 128];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t *buf = bufs[w];
+    const uint32_t nb = ctr[3];
+    for (uint32_t t = blockIdx.x * 4 + w; t < nb; t += gridDim.x * 4) {
+        const SbBig B = bigs[t];
+        const SbStream T = sb_stream((uint64_t)src, handles, out, B.i);
+        uint32_t P = 0, bb = ~0u;
+        uint64_t D = 0;
+        bool bad = false;
+        for (uint32_t k = 0; k < B.nseg && !bad; k++) {
+            const uint32_t x0 = k * kSbSeg, x1 = min(x0 + kSbSeg, T.slen);
+            if (lane == 0) segent[B.seg0 + k] = uint2{P, (uint32_t)D};
+            if (P - x0 < 64u) {  // (P >= x0: the previous segment's chain ended at or past x0)
+                const uint2 r = res[(uint64_t)(B.seg0 + k) * 64 + (P - x0)];
+                if (r.x == ~0u) bad = true;
+                P = r.x;
+                D += r.y;
+            } else {
+                // the chain from P, in windows that end at the marks as k_sb_seg's do, until it meets
+                // chain 0 of the segment at a checkpoint (then chain 0's exit is the block's) or ends
+                const uint64_t sj = (uint64_t)(B.seg0 + k);
+                while (P < x1) {
+                    if (bb == ~0u || P + 64 + 8 > bb + kSbBuf) sb_stage(buf, T, bb = P, lane);
+                    const uint32_t nm = x0 + ((P - x0) / kSbMark + 1) * kSbMark;
+                    const uint32_t lim = min(min(64u, x1 - P), nm - P);
+                    const SbWin W = sb_window(buf, bb, P, lim, T.slen, T.dlen, lane);
+                    const uint32_t wx = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.nx);
+                    if (wx >= kSbBad) { bad = true; break; }
+                    D += (uint32_t)__builtin_amdgcn_readfirstlane((int)W.sm);
+                    P += wx;
+                    if (P >= nm && P < x1) {
+                        const uint2 c = ck[sj * kSbMarks + (P - x0) / kSbMark];
+                        if (c.x == P) {  // the same element: from here on the chains are one
+                            const uint2 r0 = res[sj * 64];
+                            if (r0.x == ~0u) { bad = true; break; }
+                            D += r0.y - c.y;
+                            P = r0.x;
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        bad = bad || P != T.slen || D != T.dlen;
+        const uint32_t m_last = (T.dlen - 1) / kSbChunk, k_res = T.dlen / kSbChunk + 1;
+        // every slot unused until k_sb_emit writes it (and for good, on a failed block)
+        for (uint32_t q = lane; q < k_res; q += 64) ent[B.b0 + q] = SbEnt{~0u, 0, 0, 0};
+        if (lane == 0) {
+            if (bad) {
+                blk[2 * B.i] = 0;
+                blk[2 * B.i + 1] = 1;  // k_sb_emit skips the block
+                ser[atomicAdd(ctr + 1, 1u)] = B.i;
+            } else {
+                blk[2 * B.i] = m_last + 1;
+                blk[2 * B.i + 1] = 0;
+            }
+        }
+        sl_wsync();
+        if (!bad && lane == 0) ent[B.b0] = SbEnt{B.i, 0, 0, m_last == 0 ? 1u : 0u};
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sb_emit(const uint8_t *__restrict__ src, const bhg_handle *__restrict__ handles,
+                                                 const bhg_desc *__restrict__ out, const uint32_t *__restrict__ ctr,
+                                                 SbEnt *__restrict__ ent, const uint32_t *__restrict__ blk,
+                                                 const SbBig *__restrict__ bigs, const uint32_t *__restrict__ segblk,
+                                                 uint64_t segcap, const uint2 *__restrict__ segent) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[4][kSbBuf + 128];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t *buf = bufs[w];
+    const uint64_t total = ctr[2] < segcap ? ctr[2] : segcap;
+    for (uint64_t j = (uint64_t)blockIdx.x * 4 + w; j < total; j += (uint64_t)gridDim.x * 4) {
+        const uint32_t sb = segblk[j];
+        if (sb == ~0u) continue;
+        const SbBig B = bigs[sb];
+        if (blk[2 * B.i + 1]) continue;  // the stitch failed: the block is on the serial list
+        const SbStream T = sb_stream((uint64_t)src, handles, out, B.i);
+        const uint32_t k = (uint32_t)(j - B.seg0), x1 = min(k * kSbSeg + kSbSeg, T.slen);
+        const uint32_t m_last = (T.dlen - 1) / kSbChunk;
+        const uint2 en = segent[j];
+        uint32_t e = en.x, d = en.y, bb = ~0u;
+        uint32_t nextb = (d / kSbChunk + 1) * kSbChunk;  // the next multiple of 64 KiB above d
+        while (e < x1) {
+            if (bb == ~0u || e + 64 + 8 > bb + kSbBuf) sb_stage(buf, T, bb = e, lane);
+            const uint32_t lim = min(64u, x1 - e);
+            const SbWin W = sb_window(buf, bb, e, lim, T.slen, T.dlen, lane);
+            const uint32_t wx = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.nx);
+            const uint32_t ws = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.sm);
+            if (wx >= kSbBad) break;  // (cannot happen: the stitch walked this chain)
+            if (d + ws < nextb) {
+                d += ws;
+                e += wx;
+                continue;
+            }
+            uint32_t q = 0;
+            while (q < lim) {
+                const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)W.elen, (int)q);
+                const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)W.olen, (int)q);
+                if (el == 0) break;  // (cannot happen, as above)
+                d += ol;
+                q += el;
+                for (; nextb <= d && nextb / kSbChunk <= m_last; nextb += kSbChunk) {
+                    const uint32_t m = nextb / kSbChunk;
+                    if (lane == 0) ent[B.b0 + m] = SbEnt{B.i, e + q, d, m == m_last ? 1u : 0u};
+                }
+            }
+            if (q < lim) break;
+            e += q;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_sb_walk(const uint8_t *__restrict__ src, uint64_t src_len,
                                                  const bhg_handle *__restrict__ handles, bhg_desc *__restrict__ out,
                                                  uint8_t *__restrict__ out_vals, uint64_t out_cap,
                                                  const uint64_t *__restrict__ val_off, uint32_t *__restrict__ ctr,
                                                  const SbEnt *__restrict__ ent, uint64_t cap, uint32_t *__restrict__ blk,
-                                                 uint32_t *__restrict__ ser) {
+                                                 uint32_t *__restrict__ ser, uint32_t lpw) {
     const uint64_t base = (uint64_t)src, end = base + src_len, oend = (uint64_t)out_vals + out_cap;
     const uint64_t total = *ctr < cap ? *ctr : cap;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane >= lpw) return;
+    const uint64_t wv = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwv = (uint64_t)gridDim.x * blockDim.x / 64;
+    for (uint64_t g = wv * lpw + lane; g < total; g += nwv * lpw) {
         const SbEnt E = ent[g];
         if (E.i == ~0u) continue;
         const uint32_t i = E.i;
@@ -981,11 +1244,21 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         // then the blocks the tiers handed on (too big for a slot, or an in-place spill): chunk-parallel
         // (k_sb_parse, k_sb_walk), and lane per block from global memory for the ones that need it
         const SbScratch B = sb_layout(big, n, out_cap);
-        if (hipError_t e = hipMemsetAsync(B.ctr, 0, 8, L.stream)) return e;
+        if (hipError_t e = hipMemsetAsync(B.ctr, 0, 16, L.stream)) return e;
         hipLaunchKernelGGL(k_sb_parse, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, n, out, out_cap,
-                           val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt, B.ctr, B.ent, B.cap, B.blk, B.ser);
-        hipLaunchKernelGGL(k_sb_walk, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, out, out_vals, out_cap,
-                           val_off, B.ctr, B.ent, B.cap, B.blk, B.ser);
+                           val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt, B.ctr, B.ent, B.cap, B.blk, B.ser,
+                           B.bigs, B.segblk, B.segcap);
+        hipLaunchKernelGGL(k_sb_seg, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
+                           B.bigs, B.segblk, B.segcap, B.res, B.ck);
+        hipLaunchKernelGGL(k_sb_stitch, dim3(L.num_cus), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
+                           B.ent, B.blk, B.ser, B.bigs, B.segcap, B.segent, B.res, (const uint2 *)B.ck);
+        hipLaunchKernelGGL(k_sb_emit, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
+                           B.ent, B.blk, B.bigs, B.segblk, B.segcap, B.segent);
+        // 8 chunks per wave (the lanes of a wave walk different chunks, each element step runs every
+        // lane's path): 64 / 16 / 8 / 4 measured 25.8 / 24.8 / 24.2 / 26.8 ms per bigval step
+        // (profiles/r6/bigval/walk_lanes.txt)
+        hipLaunchKernelGGL(k_sb_walk, dim3(L.num_cus * 8), dim3(256), 0, L.stream, src, src_len, h, out, out_vals, out_cap,
+                           val_off, B.ctr, B.ent, B.cap, B.blk, B.ser, kSbLanes);
         hipLaunchKernelGGL(k_snappy_rt, dim3(L.num_cus), dim3(256), 0, L.stream, src, src_len, h, n, out, out_vals,
                            out_cap, val_off, (const uint32_t *)(B.ctr + 1), (const uint32_t *)B.ser);
         return hipGetLastError();

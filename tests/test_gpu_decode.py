@@ -359,6 +359,84 @@ def test_snappy_big_blocks_chunked(codec, seed):
         assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
 
 
+def _lit_runs(rng, data, lo, hi):
+    """data as literals of rng lengths in [lo, hi]."""
+    out, j = [], 0
+    while j < len(data):
+        k = min(len(data) - j, rng.randint(lo, hi))
+        out.append(_lit_any(data[j:j + k]))
+        j += k
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_snappy_segment_parse(codec, seed):
+    """Streams longer than 32 KiB are parsed in 16-KiB segments (k_sb_seg: 64 speculative chains
+    per segment, k_sb_stitch: the block's chain through them, k_sb_emit: the 64-KiB chunk slots).
+    Cases: golang-encoded compressible values of 100 KiB - 2 MiB; literals of 65-300 B (a literal
+    over a segment start: the stitch walks that segment itself); streams of 1-byte literals (stream
+    twice the output: more segments than the scratch holds, so some blocks take the one-wave parse);
+    a 200-KiB literal (one element over three 64-KiB output boundaries: empty chunks); a copy
+    offset past the output in a late segment, a literal length past the stream, a trailing extra
+    byte (irregular: serial pass); stream lengths at the 32-KiB edge."""
+    rng = random.Random(seed)
+    g = np.random.default_rng(seed)
+    streams = []
+    for sz in [100000, 300000, (1 << 20) + 3, 2 << 20]:
+        streams.append(O.snappy_encode(compressible(rng, sz)))
+    for _ in range(6):
+        d = np_bytes(g, rng.choice([70000, 150000, 400000]))
+        st = _lit_runs(rng, d, 65, 300)
+        streams.append(_uvarint(len(d)) + st)
+    for _ in range(40):  # 1-byte literals: 2 stream bytes per output byte
+        d = np_bytes(g, rng.choice([66000, 120000, 250000]))
+        streams.append(_uvarint(len(d)) + b"".join(bytes([0]) + d[j:j + 1] for j in range(len(d))))
+    d = np_bytes(g, 200000)
+    streams.append(_uvarint(200000 + 64) + _lit_any(d) + _copy2(1000, 64))
+    for edge in [32767, 32768, 32769, 32770]:  # stream lengths (after the uvarint) around kSbSegMin
+        body = _lit_any(np_bytes(g, 1000))
+        y = 2 * (edge - len(body)) % 3  # 3 x + 2 y = the rest
+        x = (edge - len(body) - 2 * y) // 3
+        body += _copy2(1000, 64) * x + bytes([(11 - 4) << 2 | 1, 100]) * y  # copy-2s, then copy-1s of 11 B
+        assert len(body) == edge
+        streams.append(_uvarint(1000 + 64 * x + 11 * y) + body)
+    base = O.snappy_encode(compressible(rng, 600000))
+    lastcp = len(base) - 200
+    while base[lastcp] & 3 != 2:
+        lastcp += 1
+    b1 = bytearray(base)
+    b1[lastcp + 1:lastcp + 3] = (0xffff).to_bytes(2, "little")  # copy offset past the output written
+    streams.append(bytes(b1))
+    d = np_bytes(g, 80000)
+    streams.append(_uvarint(80000) + _lit_any(d)[:-10])               # literal past the stream
+    streams.append(O.snappy_encode(compressible(rng, 90000)) + b"\x00")  # extra byte after dlen
+    small = [O.snappy_encode(compressible(rng, rng.choice([16, 900, 3000]))) for _ in range(100)]
+    allst = streams + small
+    rng.shuffle(allst)
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(allst):
+        rec = O.record_set(b"seg%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    # a batch of long records (mean past 8 KiB): the header pass leaves the records over 16 KiB to
+    # the long-record CRC pass; expected CRCs with every 7th flipped check its status
+    assert len(src) > 8192 * len(h)
+    e0, _, _ = O.decode_batch(bytes(src), h, codec=1)
+    ecrc = e0["crc"].astype(np.uint32).copy()
+    ecrc[::7] ^= 1
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1, expected_crc=ecrc)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1, expected_crc=ecrc)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    assert (exp["status"] == O.CRC_MISMATCH).sum() >= len(h) // 7 - 6
+    ok = np.nonzero((exp["status"] == O.OK) | (exp["status"] == O.CRC_MISMATCH))[0]
+    assert len(ok) >= len(allst) - 6
+    for i in ok:
+        assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
+
+
 def test_snappy_long_streams_in_lds(codec):
     """Streams longer than the 64 chunks a lane-per-chunk staging covers (1,025 .. 1,064 B
     for a <= 1 KiB value: values snappy cannot shrink) are decoded in their LDS slot, the
