@@ -763,13 +763,14 @@ struct SbBig {
 static size_t al256_(size_t x) { return (x + 255) & ~(size_t)255; }
 static uint64_t sb_cap(uint32_t n, uint64_t out_cap) { return out_cap / kSbChunk + n + 1; }
 static uint64_t sb_segcap(uint32_t n, uint64_t out_cap) { return out_cap / kSbSeg + n + 1; }
-constexpr uint32_t kSbMark = 1024;              // checkpoint spacing of chain 0 in a segment
-constexpr uint32_t kSbMarks = kSbSeg / kSbMark; // checkpoints per segment (index 0 unused)
+constexpr uint32_t kSbMark = 1024;              // checkpoint spacing along a chain of a segment
+constexpr uint32_t kSbMarks = kSbSeg / kSbMark; // checkpoints per chain (index 0 unused)
+constexpr uint32_t kSbCk = 4;                    // chains with checkpoints: lanes 0, 16, 32, 48
 size_t snappy_big_bytes(uint32_t n, uint64_t out_cap) {
     const uint64_t sc = sb_segcap(n, out_cap);
     return 256 + al256_(sb_cap(n, out_cap) * sizeof(SbEnt)) + al256_((size_t)n * 8) + al256_((size_t)n * 4) +
            al256_((size_t)n * sizeof(SbBig)) + al256_(sc * 4) + al256_(sc * 8) + al256_(sc * 64 * 8) +
-           al256_(sc * kSbMarks * 8);
+           al256_(sc * kSbCk * kSbMarks * 8);
 }
 struct SbScratch {
     uint32_t *ctr;
@@ -1018,9 +1019,10 @@ __global__ __launch_bounds__(256) void k_sb_seg(const uint8_t *__restrict__ src,
         const SbBig B = bigs[sb];
         const SbStream T = sb_stream((uint64_t)src, handles, out, B.i);
         const uint32_t k = (uint32_t)(j - B.seg0), x0 = k * kSbSeg, x1 = min(x0 + kSbSeg, T.slen);
-        uint32_t P = x0 + lane, O = 0, bb = ~0u, cn = 1;  // cn: chain 0's next checkpoint (lane 0)
+        uint32_t P = x0 + lane, O = 0, bb = ~0u, cn = 1;  // cn: the chain's next checkpoint (lanes 16 q)
         bool act = P < x1;
-        uint2 *const ckj = ck + j * kSbMarks;
+        const bool ckl = (lane & 15) == 0;
+        uint2 *const ckj = ck + (j * kSbCk + (lane >> 4)) * kSbMarks;
         for (;;) {
             const uint32_t key = act ? P : ~0u;
             const uint32_t E = ~(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(~key), 63);  // the lowest chain
@@ -1042,12 +1044,12 @@ __global__ __launch_bounds__(256) void k_sb_seg(const uint8_t *__restrict__ src,
                     P = E + nx;
                     O += sm;
                     act = P < x1;
-                    // chain 0 at every mark it reaches: its first element at or past the mark
-                    for (; lane == 0 && cn < kSbMarks && P >= x0 + cn * kSbMark; cn++) ckj[cn] = uint2{P, O};
+                    // chains 0, 16, 32, 48 at every mark they reach: their first element at or past it
+                    for (; ckl && cn < kSbMarks && P >= x0 + cn * kSbMark; cn++) ckj[cn] = uint2{P, O};
                 }
             }
         }
-        for (; lane == 0 && cn < kSbMarks; cn++) ckj[cn] = uint2{~0u, 0};
+        for (; ckl && cn < kSbMarks; cn++) ckj[cn] = uint2{~0u, 0};
         res[j * 64 + lane] = uint2{P, O};  // P = ~0: an irregular element on the chain from x0 + lane
     }
 }
@@ -1068,19 +1070,44 @@ __global__ __launch_bounds__(256) void k_sb_stitch(const uint8_t *__restrict__ s
         uint32_t P = 0, bb = ~0u;
         uint64_t D = 0;
         bool bad = false;
+        // the chain results of the next kSbPf segments in flight, lane b holding chain b's (a step
+        // is then a v_readlane, not a memory round trip: 0.73 -> ms per bigval step)
+        constexpr uint32_t kSbPf = 4;
+#ifdef BHG_SB_PROF
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        uint32_t nmiss = 0, nwin = 0, nmerge = 0;
+#endif
+        uint2 rr[kSbPf];
+#pragma unroll
+        for (uint32_t q = 0; q < kSbPf; q++)
+            rr[q] = res[(uint64_t)(B.seg0 + (q < B.nseg ? q : 0u)) * 64 + lane];
         for (uint32_t k = 0; k < B.nseg && !bad; k++) {
             const uint32_t x0 = k * kSbSeg, x1 = min(x0 + kSbSeg, T.slen);
+            const uint2 rk = rr[0];
+#pragma unroll
+            for (uint32_t q = 0; q + 1 < kSbPf; q++) rr[q] = rr[q + 1];
+            rr[kSbPf - 1] = res[(uint64_t)(B.seg0 + (k + kSbPf < B.nseg ? k + kSbPf : 0u)) * 64 + lane];
             if (lane == 0) segent[B.seg0 + k] = uint2{P, (uint32_t)D};
             if (P - x0 < 64u) {  // (P >= x0: the previous segment's chain ended at or past x0)
-                const uint2 r = res[(uint64_t)(B.seg0 + k) * 64 + (P - x0)];
+                const uint32_t b = P - x0;
+                const uint2 r = {(uint32_t)__builtin_amdgcn_readlane((int)rk.x, (int)b),
+                                 (uint32_t)__builtin_amdgcn_readlane((int)rk.y, (int)b)};
                 if (r.x == ~0u) bad = true;
                 P = r.x;
                 D += r.y;
             } else {
                 // the chain from P, in windows that end at the marks as k_sb_seg's do, until it meets
-                // chain 0 of the segment at a checkpoint (then chain 0's exit is the block's) or ends
+                // one of the segment's checkpointed chains at a mark (then that chain's exit is the
+                // block's) or ends.  (Four chains: a chain from inside a long literal's bytes parses
+                // them as tags and can die on a garbage length before it meets the block's.)
                 const uint64_t sj = (uint64_t)(B.seg0 + k);
+#ifdef BHG_SB_PROF
+                nmiss++;
+#endif
                 while (P < x1) {
+#ifdef BHG_SB_PROF
+                    nwin++;
+#endif
                     if (bb == ~0u || P + 64 + 8 > bb + kSbBuf) sb_stage(buf, T, bb = P, lane);
                     const uint32_t nm = x0 + ((P - x0) / kSbMark + 1) * kSbMark;
                     const uint32_t lim = min(min(64u, x1 - P), nm - P);
@@ -1090,12 +1117,20 @@ __global__ __launch_bounds__(256) void k_sb_stitch(const uint8_t *__restrict__ s
                     D += (uint32_t)__builtin_amdgcn_readfirstlane((int)W.sm);
                     P += wx;
                     if (P >= nm && P < x1) {
-                        const uint2 c = ck[sj * kSbMarks + (P - x0) / kSbMark];
-                        if (c.x == P) {  // the same element: from here on the chains are one
-                            const uint2 r0 = res[sj * 64];
-                            if (r0.x == ~0u) { bad = true; break; }
-                            D += r0.y - c.y;
-                            P = r0.x;
+                        // lane q: checkpoint set q's entry at this mark
+                        const uint2 c = ck[((uint64_t)sj * kSbCk + (lane < kSbCk ? lane : 0u)) * kSbMarks + (P - x0) / kSbMark];
+                        const uint64_t hit = __ballot(lane < kSbCk && c.x == P);
+                        if (hit) {  // the same element: from here on the chains are one
+#ifdef BHG_SB_PROF
+                            nmerge++;
+#endif
+                            const uint32_t q = (uint32_t)__builtin_ctzll(hit);
+                            const uint32_t cy = (uint32_t)__builtin_amdgcn_readlane((int)c.y, (int)q);
+                            const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)rk.x, (int)(16 * q));
+                            const uint32_t ey = (uint32_t)__builtin_amdgcn_readlane((int)rk.y, (int)(16 * q));
+                            if (ex == ~0u) { bad = true; break; }
+                            D += ey - cy;
+                            P = ex;
                             break;
                         }
                     }
@@ -1103,6 +1138,12 @@ __global__ __launch_bounds__(256) void k_sb_stitch(const uint8_t *__restrict__ s
             }
         }
         bad = bad || P != T.slen || D != T.dlen;
+#ifdef BHG_SB_PROF
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && t1 - t0 > 20000)
+            printf("stitch blk %u nseg %u miss %u win %u merge %u bad %d cycles %llu\n", B.i, B.nseg, nmiss, nwin, nmerge,
+                   (int)bad, (unsigned long long)(t1 - t0));
+#endif
         const uint32_t m_last = (T.dlen - 1) / kSbChunk, k_res = T.dlen / kSbChunk + 1;
         // every slot unused until k_sb_emit writes it (and for good, on a failed block)
         for (uint32_t q = lane; q < k_res; q += 64) ent[B.b0 + q] = SbEnt{~0u, 0, 0, 0};
@@ -1248,11 +1289,14 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         hipLaunchKernelGGL(k_sb_parse, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, n, out, out_cap,
                            val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt, B.ctr, B.ent, B.cap, B.blk, B.ser,
                            B.bigs, B.segblk, B.segcap);
-        hipLaunchKernelGGL(k_sb_seg, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
+        // 8 workgroups of 4 waves per CU for the segment parse and the emit (window steps are
+        // latency-bound: 4 per CU measured 11.36 vs 10.77 ms per bigval step, profiles/r6/bigval/)
+        constexpr uint32_t sbw = 8;
+        hipLaunchKernelGGL(k_sb_seg, dim3(L.num_cus * sbw), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
                            B.bigs, B.segblk, B.segcap, B.res, B.ck);
         hipLaunchKernelGGL(k_sb_stitch, dim3(L.num_cus), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
                            B.ent, B.blk, B.ser, B.bigs, B.segcap, B.segent, B.res, (const uint2 *)B.ck);
-        hipLaunchKernelGGL(k_sb_emit, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
+        hipLaunchKernelGGL(k_sb_emit, dim3(L.num_cus * sbw), dim3(256), 0, L.stream, src, h, (const bhg_desc *)out, B.ctr,
                            B.ent, B.blk, B.bigs, B.segblk, B.segcap, B.segent);
         // 8 chunks per wave (the lanes of a wave walk different chunks, each element step runs every
         // lane's path): 64 / 16 / 8 / 4 measured 25.8 / 24.8 / 24.2 / 26.8 ms per bigval step
