@@ -37,7 +37,7 @@ if [ -n "$BENCH" ]; then
 fi
 if [ -n "$ABENV" ]; then
   for r in $(seq 1 ${ABN:-3}); do
-    for v in 0 1; do
+    for v in ${ABVALS:-0 1}; do
       f=$O/abenv_${v}_$r.json
       env $ABENV=$v timeout -k 10 300 python3 -u bench.py $ABARGS > $f 2> $f.err || { tail -20 $f.err; exit 1; }
       python3 -c "import json; d=json.load(open('$f')); print('$ABENV=$v run $r', d['value'], d['ms_per_step'])"
