@@ -410,8 +410,14 @@ __device__ __forceinline__ SlInfo sl_finish(const SlRaw &w, uint32_t n, uint64_t
 // The element decode is straight-line (selects, non-short-circuit checks) so
 // the 64 lanes of a wave do not split into per-tag-type paths; the tag read is
 // unconditional (a read at se lies inside the slot).
+// G lanes per block (lane g of its group): all G decode the same elements; a literal or a copy that
+// does not overlap its own output (offset >= length) moves its 16-B ops G at a time, one per lane
+// (they read only bytes below the element's output, or the stream); an overlapping copy runs its
+// ops one after another on every lane of the group (the same addresses and bytes).  The lanes of a
+// group hand bytes to each other through LDS in the wave's program order.
+template <int G>
 __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op,
-                                                    uint32_t dlen) {
+                                                    uint32_t dlen, uint32_t g) {
     uint32_t s = sp, d = 0, res = 0;
     // the tag and the 4 bytes after it (one unaligned ds_read_b64; two aligned dword reads
     // measured no faster)
@@ -460,12 +466,17 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
         // n >= 1 here (n == 0 is `bad`): a do-while, so the compiler sees that the next tag's read
         // (issued before the first op's read, which the op waits for) is complete at the loop head
         // and does not wait there for the last op's write as well
-        uint32_t t = 0, r = 0;
-        do {
-            *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
-            t += dstep;
-            r += sstep;
-        } while (t < n);
+        if (G > 1 && (mlit | (0u - (uint32_t)(off >= n))) != 0u) {
+            for (uint32_t t = 16 * g; t < n; t += 16 * G)
+                *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + t);
+        } else {
+            uint32_t t = 0, r = 0;
+            do {
+                *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + r);
+                t += dstep;
+                r += sstep;
+            } while (t < n);
+        }
         d += n;
         s = sn;
         t8 = t8n;
@@ -499,7 +510,7 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 // neither carries the other's code)
 // the work of one slot shape over its list (a "role"): lds holds BPW * SLOT + 64 bytes (+ 64:
 // literal reads past the last slot); the workgroup takes groups blockIdx.x, + gridDim.x, ...
-template <int BPW, int SLOT, int CH, int ORDER, int NSUB>
+template <int BPW, int SLOT, int CH, int ORDER, int NSUB, int GL = 1>
 __device__ __forceinline__ void sl_role(uint8_t *__restrict__ lds, const uint8_t *__restrict__ src, uint64_t src_len,
                                         const bhg_handle *__restrict__ handles, uint32_t n,
                                         bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals, uint64_t out_cap,
@@ -639,15 +650,38 @@ __device__ __forceinline__ void sl_role(uint8_t *__restrict__ lds, const uint8_t
         prefetch(nxt);
         // 3. decode
         uint32_t fin = cur.status, mode = cur.mode;
-        if (mode == SL_LDS) {
-            const uint32_t sb = lane * SLOT, sp = sb + sl_pos<SLOT>(cur.clen);
-            uint32_t hdr = 0;
-            while (hdr < 5 && lds[sp + hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
-            hdr++;
-            const uint32_t r = snappy_walk_lds(lds, sp + hdr, sp + cur.clen, sb, cur.dlen);
-            if (r == 1) fin = BHG_ST_SNAPPY_CORRUPT;
-            if (r == 2) mode = SL_GLOBAL;
-        } else if (mode == SL_TOOLARGE) {
+        if (GL == 1) {
+            if (mode == SL_LDS) {
+                const uint32_t sb = lane * SLOT, sp = sb + sl_pos<SLOT>(cur.clen);
+                uint32_t hdr = 0;
+                while (hdr < 5 && lds[sp + hdr] >= 0x80) hdr++;  // uvarint decodedLen, validated by the header pass
+                hdr++;
+                const uint32_t r = snappy_walk_lds<1>(lds, sp + hdr, sp + cur.clen, sb, cur.dlen, 0);
+                if (r == 1) fin = BHG_ST_SNAPPY_CORRUPT;
+                if (r == 2) mode = SL_GLOBAL;
+            }
+        } else {
+            // lane l walks block l / G (its fields from lane l / G), then lane b < BPW takes block b's
+            // result from its group's first lane
+            static_assert(BPW * GL <= 64, "groups fit the wave");
+            const uint32_t bl = lane / GL;
+            const uint32_t gm = (uint32_t)__shfl((int)mode, (int)bl, 64), gc = (uint32_t)__shfl((int)cur.clen, (int)bl, 64);
+            const uint32_t gd = (uint32_t)__shfl((int)cur.dlen, (int)bl, 64);
+            uint32_t r = 0;
+            if (bl < (uint32_t)BPW && gm == SL_LDS) {
+                const uint32_t sb = bl * SLOT, sp = sb + sl_pos<SLOT>(gc);
+                uint32_t hdr = 0;
+                while (hdr < 5 && lds[sp + hdr] >= 0x80) hdr++;
+                hdr++;
+                r = snappy_walk_lds<GL>(lds, sp + hdr, sp + gc, sb, gd, lane % GL);
+            }
+            r = (uint32_t)__shfl((int)r, (int)(lane * GL < 64 ? lane * GL : 0u), 64);
+            if (mode == SL_LDS) {
+                if (r == 1) fin = BHG_ST_SNAPPY_CORRUPT;
+                if (r == 2) mode = SL_GLOBAL;
+            }
+        }
+        if (mode == SL_TOOLARGE) {
             fin = BHG_ST_SNAPPY_TOO_LARGE;
         }
         // 4. decoded blocks -> out_vals
@@ -685,6 +719,7 @@ __device__ __forceinline__ void sl_role(uint8_t *__restrict__ lds, const uint8_t
 }
 
 // tier 1 in the batch's own order (when >= 7/8 of the blocks are small; else it returns at once)
+template <int G1>
 __global__ __launch_bounds__(64) void k_snappy_lds_nat(const uint8_t *__restrict__ src, uint64_t src_len,
                                                        const bhg_handle *__restrict__ handles, uint32_t n,
                                                        bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
@@ -693,7 +728,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds_nat(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ e_small, uint32_t sub_cap,
                                                        uint32_t *__restrict__ c_rt, uint32_t *__restrict__ e_rt) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kSlBpw * kSlSlot + 64];
-    sl_role<kSlBpw, kSlSlot, 1, 2, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
+    sl_role<kSlBpw, kSlSlot, 1, 2, 64, G1>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
                                        sub_cap, c_rt, e_rt);
 }
 
@@ -702,6 +737,7 @@ __global__ __launch_bounds__(64) void k_snappy_lds_nat(const uint8_t *__restrict
 // empty roles of an all-1-KiB batch cost one start-up, and a role's tail overlaps the next one's
 // groups.
 constexpr uint32_t kMultiLds = 23 * 1088 + 64;  // the largest role (6 x 4,160 + 64 = 25,024 B is next)
+template <int G1, int G2>
 __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restrict__ src, uint64_t src_len,
                                                          const bhg_handle *__restrict__ handles, uint32_t n,
                                                          bhg_desc *__restrict__ out, uint8_t *__restrict__ out_vals,
@@ -716,15 +752,15 @@ __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restri
     const uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * sub_cap;
     uint32_t *e_rt = list + kSnapListHdr + (size_t)kSnapSubs * sub_cap;
     const size_t bs = (size_t)64 * sub_cap;
-    sl_role<6, 4160, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large, e_large, sub_cap,
+    sl_role<6, 4160, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large, e_large, sub_cap,
                                c_rt, e_rt);
-    sl_role<7, 3392, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 64,
+    sl_role<7, 3392, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 64,
                                e_large + bs, sub_cap, c_rt, e_rt);
-    sl_role<9, 2624, 2, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 128,
+    sl_role<9, 2624, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 128,
                                e_large + 2 * bs, sub_cap, c_rt, e_rt);
-    sl_role<13, 1856, 1, 0, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 192,
+    sl_role<13, 1856, 1, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 192,
                                 e_large + 3 * bs, sub_cap, c_rt, e_rt);
-    sl_role<23, 1088, 1, 1, 64>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
+    sl_role<23, 1088, 1, 1, 64, G1>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
                                 sub_cap, c_rt, e_rt);
 }
 
@@ -1265,21 +1301,26 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         const uint32_t cap = (uint32_t)snappy_sub_cap(n);
         uint32_t *c_small = list, *c_rt = list + kSnapRtCount;
         uint32_t *e_small = list + kSnapListHdr, *e_rt = list + kSnapListHdr + (size_t)kSnapSubs * cap;
+        // lanes per block: 2 in tier 1, 4 in tier 2 (snappy_walk_lds).  One lane per block in both:
+        // C3 589.5 / mixdec 251.3 GiB/s; 2 / 4: 594.0 / 286.3; 1 / 4: 591.1 / 286.6; 2 / 2: 576 / 263.6
+        // (2 alternating runs each, profiles/r6/slg/)
+        constexpr int kG1 = 2, kG2 = 4;
         {
             static const uint32_t per_cu =
-                resident_per_cu((const void *)k_snappy_lds_nat, 64, (160u * 1024u) / (kSlBpw * kSlSlot + 64));
+                resident_per_cu((const void *)k_snappy_lds_nat<kG1>, 64, (160u * 1024u) / (kSlBpw * kSlSlot + 64));
             const uint32_t groups = (n + kSlBpw - 1) / kSlBpw, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
             const uint32_t grid = groups < lim ? (groups ? groups : 1u) : lim;
-            hipLaunchKernelGGL(k_snappy_lds_nat, dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out, out_vals,
+            hipLaunchKernelGGL(k_snappy_lds_nat<kG1>, dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out, out_vals,
                                out_cap, val_off, c_small, e_small, cap, c_rt, e_rt);
             if (hipError_t e = hipGetLastError()) return e;
         }
         {
-            static const uint32_t per_cu = resident_per_cu((const void *)k_snappy_lds_multi, 64, (160u * 1024u) / kMultiLds);
+            static const uint32_t per_cu =
+                resident_per_cu((const void *)k_snappy_lds_multi<kG1, kG2>, 64, (160u * 1024u) / kMultiLds);
             const uint32_t groups = (n + 5) / 6, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
             const uint32_t grid = groups < lim ? (groups ? groups : 1u) : lim;
-            hipLaunchKernelGGL(k_snappy_lds_multi, dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out, out_vals,
-                               out_cap, val_off, list, cap);
+            hipLaunchKernelGGL((k_snappy_lds_multi<kG1, kG2>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
+                               out_vals, out_cap, val_off, list, cap);
             if (hipError_t e = hipGetLastError()) return e;
         }
         // then the blocks the tiers handed on (too big for a slot, or an in-place spill): chunk-parallel
