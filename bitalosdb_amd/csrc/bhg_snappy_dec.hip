@@ -1304,7 +1304,8 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         // lanes per block: 2 in tier 1, 4 in tier 2 (snappy_walk_lds).  One lane per block in both:
         // C3 589.5 / mixdec 251.3 GiB/s; 2 / 4: 594.0 / 286.3; 1 / 4: 591.1 / 286.6; 2 / 2: 576 / 263.6
         // (2 alternating runs each, profiles/r6/slg/)
-        constexpr int kG1 = 2, kG2 = 4;
+        constexpr int kG1 = 2;
+        constexpr int kG2 = 4;
         {
             static const uint32_t per_cu =
                 resident_per_cu((const void *)k_snappy_lds_nat<kG1>, 64, (160u * 1024u) / (kSlBpw * kSlSlot + 64));

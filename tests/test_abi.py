@@ -101,8 +101,14 @@ def test_shipped_library_has_default_knobs():
         rb"_ZN3bhg13k_decode_tileI": {b"_ZN3bhg13k_decode_tileILi8ELi%dELi%dELi2ELi%dEE" % (nch, pf, lg)
                                       for lg in (0, 1)},
     }
-    # the snappy LDS tiers: tier 1 in batch order, and one multi-role launch for the lists
-    assert b"_ZN3bhg16k_snappy_lds_natE" in blob and b"_ZN3bhg18k_snappy_lds_multiE" in blob
+    # the snappy LDS tiers: tier 1 in batch order, and one multi-role launch for the lists, with
+    # kG1 / kG2 lanes per block
+    g1 = _src_default("bhg_snappy_dec.hip", "kG1")
+    g2 = _src_default("bhg_snappy_dec.hip", "kG2")
+    nat = set(re.findall(rb"_ZN3bhg16k_snappy_lds_natI[A-Za-z0-9]+?EE", blob))
+    multi = set(re.findall(rb"_ZN3bhg18k_snappy_lds_multiI[A-Za-z0-9]+?EE", blob))
+    assert nat == {b"_ZN3bhg16k_snappy_lds_natILi%dEE" % g1}, nat
+    assert multi == {b"_ZN3bhg18k_snappy_lds_multiILi%dELi%dEE" % (g1, g2)}, multi
     assert not re.search(rb"_ZN3bhg12k_snappy_ldsI", blob)
     assert _src_default("bhg_snappy_dec.hip", "kSlBpw") == 18 and slot == 1088
     for prefix, names in want.items():
