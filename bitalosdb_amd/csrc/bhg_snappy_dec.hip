@@ -414,7 +414,11 @@ __device__ __forceinline__ SlInfo sl_finish(const SlRaw &w, uint32_t n, uint64_t
 // does not overlap its own output (offset >= length) moves its 16-B ops G at a time, one per lane
 // (they read only bytes below the element's output, or the stream); an overlapping copy runs its
 // ops one after another on every lane of the group (the same addresses and bytes).  The lanes of a
-// group hand bytes to each other through LDS in the wave's program order.
+// group hand bytes to each other through LDS in the wave's program order: a round of the parallel
+// loop is one read instruction, then one write instruction, for all G lanes -- a literal in an
+// in-place slot reads its stream just above the output it writes, so its round k + 1 reads bytes
+// at or above where round k wrote only because every read of a round precedes the round's writes
+// (tests/test_snappy_walk_host.py runs the walk on the host in exactly this order).
 template <int G>
 __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op,
                                                     uint32_t dlen, uint32_t g) {

@@ -29,9 +29,28 @@ def walk(tmp_path_factory):
     if not os.path.exists(CLANG):
         pytest.skip("no clang++")
     s = open(SRC).read()
-    i0 = s.index("__device__ __forceinline__ uint32_t snappy_walk_lds(")
+    # the walk is a template on G (lanes per block).  On the host one call is the whole group, in
+    # the lanes' lockstep order: an element's parallel 16-B ops go in rounds of G, each round's G
+    # reads before its G writes (one ds_read, then one ds_write instruction, on the GPU).  (A literal
+    # in an in-place slot reads its stream just above the output it writes, so ops in another
+    # order would read bytes a previous op overwrote.)
+    i0 = s.index("template <int G>\n__device__ __forceinline__ uint32_t snappy_walk_lds(")
     i1 = s.index("\n}\n", i0) + 3  # the end of the function
-    body = s[i0:i1].replace("__device__ __forceinline__ ", 'extern "C" ')
+    body = s[i0:i1].replace("__device__ __forceinline__ ", "")
+    par = ("            for (uint32_t t = 16 * g; t < n; t += 16 * G)\n"
+           "                *reinterpret_cast<u32x4_lds_u *>(lds + o + t) = *reinterpret_cast<const u32x4_lds_u *>(lds + a + t);\n")
+    assert body.count(par) == 1
+    body = body.replace(par, (
+        "            for (uint32_t t0 = 0; t0 < n; t0 += 16 * G) {\n"
+        "                u32x4 tmp[G];\n"
+        "                for (uint32_t gg = 0; gg < G; gg++)\n"
+        "                    if (t0 + 16 * gg < n) tmp[gg] = *reinterpret_cast<const u32x4_lds_u *>(lds + a + t0 + 16 * gg);\n"
+        "                for (uint32_t gg = 0; gg < G; gg++)\n"
+        "                    if (t0 + 16 * gg < n) *reinterpret_cast<u32x4_lds_u *>(lds + o + t0 + 16 * gg) = tmp[gg];\n"
+        "            }\n"))
+    for gl in (1, 2, 4):
+        body += ('extern "C" uint32_t snappy_walk_lds_%d(uint8_t *lds, uint32_t sp, uint32_t se, uint32_t op, '
+                 'uint32_t dlen) { return snappy_walk_lds<%d>(lds, sp, se, op, dlen, 0); }\n' % (gl, gl))
     hdr = ("#include <stdint.h>\n"
            "#define __builtin_amdgcn_s_waitcnt(x) ((void)0)\n"   # a wait-count hint on the GPU
            "typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));\n"
@@ -42,12 +61,19 @@ def walk(tmp_path_factory):
     cpp.write_text(hdr + body)
     subprocess.check_call([CLANG, "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(so), str(cpp)])
     lib = ctypes.CDLL(str(so))
-    lib.snappy_walk_lds.restype = ctypes.c_uint32
-    lib.snappy_walk_lds.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 4
+    for gl in (1, 2, 4):
+        f = getattr(lib, "snappy_walk_lds_%d" % gl)
+        f.restype = ctypes.c_uint32
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 4
     return lib
 
 
-def run_slot(walk, stream, dlen, slot=SLOT):
+@pytest.fixture(params=[1, 2, 4])
+def lanes(request):
+    return request.param
+
+
+def run_slot(walk, stream, dlen, slot=SLOT, lanes=1):
     """Stage `stream` as k_snappy_lds does and walk it; returns (code, output bytes)."""
     clen = len(stream)
     pos = (slot - 8 - ((clen + 15) & ~15)) & ~15
@@ -57,7 +83,7 @@ def run_slot(walk, stream, dlen, slot=SLOT):
     while hdr < 5 and lds[pos + hdr] >= 0x80:
         hdr += 1
     hdr += 1
-    r = walk.snappy_walk_lds(lds.ctypes.data, pos + hdr, pos + clen, 0, dlen)
+    r = getattr(walk, "snappy_walk_lds_%d" % lanes)(lds.ctypes.data, pos + hdr, pos + clen, 0, dlen)
     return r, lds[:dlen].tobytes()
 
 
@@ -86,14 +112,14 @@ def values(rng, k):
                            bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(64))[:n]
 
 
-def test_walk_matches_restated_decode(walk):
+def test_walk_matches_restated_decode(walk, lanes):
     rng = random.Random(5)
     codes = {0: 0, 1: 0, 2: 0}
     for v in values(rng, 1500):
         st = O.snappy_encode(v)
         if len(st) + 24 > SLOT or len(v) > 1024:
             continue                       # not staged: the kernel sends it to k_snappy_rt
-        r, out = run_slot(walk, st, len(v))
+        r, out = run_slot(walk, st, len(v), lanes=lanes)
         codes[r] += 1
         assert r != 1
         if r == 0:
@@ -101,7 +127,7 @@ def test_walk_matches_restated_decode(walk):
     assert codes[0] > 1000
 
 
-def test_walk_tier2_slots(walk):
+def test_walk_tier2_slots(walk, lanes):
     """The same walk in tier 2's 4,160-B slots: values of 1-4 KiB (dict-like tokens, runs,
     incompressible) decode to the restated bytes or are handed over, never wrong."""
     rng = random.Random(9)
@@ -124,7 +150,7 @@ def test_walk_tier2_slots(walk):
         st = O.snappy_encode(v)
         if len(st) + 24 > SLOT2:
             continue
-        r, out = run_slot(walk, st, len(v), SLOT2)
+        r, out = run_slot(walk, st, len(v), SLOT2, lanes)
         codes[r] += 1
         assert r != 1
         if r == 0:
@@ -132,18 +158,18 @@ def test_walk_tier2_slots(walk):
     assert codes[0] > 250
 
 
-def test_walk_hands_over_when_output_overtakes_stream(walk):
+def test_walk_hands_over_when_output_overtakes_stream(walk, lanes):
     body = bytes([0]) + b"x"
     body += (bytes([(64 - 1) << 2 | 2]) + (1).to_bytes(2, "little")) * 10
     body += bytes([(59 - 1) << 2 | 2]) + (1).to_bytes(2, "little")
     body += (bytes([2]) + (7).to_bytes(2, "little")) * 324      # 324 one-byte copies, 3 B of stream each
     st = uvarint(1024) + body
     assert O.snappy_decode(st) is not None
-    r, _ = run_slot(walk, st, 1024)
+    r, _ = run_slot(walk, st, 1024, lanes=lanes)
     assert r == 2
 
 
-def test_walk_rejects_what_the_restatement_rejects(walk):
+def test_walk_rejects_what_the_restatement_rejects(walk, lanes):
     rng = random.Random(6)
     good = O.snappy_encode(b"".join(bytes([rng.getrandbits(8)]) * 9 for _ in range(100)))
     cases = [
@@ -164,7 +190,7 @@ def test_walk_rejects_what_the_restatement_rejects(walk):
             continue                       # rejected by the header pass before any walk
         if dl > 1024:
             continue
-        r, _ = run_slot(walk, st, dl)
+        r, _ = run_slot(walk, st, dl, lanes=lanes)
         assert r in (1, 2), st
         walked += 1
     assert walked >= 4
