@@ -5,7 +5,9 @@
 
 namespace bhg {
 
-constexpr int kStreamNch = 4;     // CRC chains per window
+// CRC chains per window: 4 / 2 chains of 128-B windows, 4 / 8 of 256-B ones measured C3 595.5 / 599.1 /
+// 566.8 / 565.0 GiB/s, mixdec 287.5 / 288.6 / 282.7 / 282.5 (2 alternating runs each, profiles/r6/stream/)
+constexpr int kStreamNch = 2;
 constexpr int kStreamWin = 128;   // window bytes
 constexpr int kStreamPipe = 0;    // software-pipelined window loads (measured no faster)
 
