@@ -12,7 +12,7 @@ struct Launch {
     hipStream_t stream;
     int num_cus;           // 256 on MI355X
     const uint32_t *ztab;  // device copy of build_tile_ztab() (owned by the context)
-    const uint32_t *stab;  // device copy of build_stream_tab(128, 4) (owned by the context)
+    const uint32_t *stab;  // device copy of build_stream_tab(kStreamWin, kStreamNch) (owned by the context)
     const uint32_t *xtab;  // device copy of build_xtab() (owned by the context)
 };
 
