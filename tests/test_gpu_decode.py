@@ -437,6 +437,49 @@ def test_snappy_segment_parse(codec, seed):
         assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
 
 
+@pytest.mark.parametrize("seed", [7, 8])
+def test_snappy_big_streams_fuzzed(codec, seed):
+    """Long golang/snappy streams (the segment parse, the chunk walk) with 1-3 bytes flipped at
+    random places, each flip a stream of its own; random bytes behind a valid uvarint of a large
+    decoded length; truncations at random points.  Every descriptor and every decoded value must
+    equal the restated decoder's -- a corrupt stream is reported, never decoded into other bytes."""
+    rng = random.Random(seed)
+    g = np.random.default_rng(seed)
+    bases = [O.snappy_encode(compressible(rng, n)) for n in (70000, 200000, 700000)]
+    bases.append(O.snappy_encode(np_bytes(g, 150000)))
+    streams = []
+    for b in bases:
+        streams.append(b)
+        for _ in range(12):
+            x = bytearray(b)
+            for _ in range(rng.randint(1, 3)):
+                x[rng.randrange(4, len(x))] ^= rng.randrange(1, 256)
+            streams.append(bytes(x))
+        for _ in range(3):
+            streams.append(b[:rng.randrange(len(b) // 2, len(b))])
+    for n in (40000, 100000, 300000):
+        streams.append(_uvarint(2 * n) + np_bytes(g, n))
+    small = [O.snappy_encode(compressible(rng, rng.choice([50, 900, 3000]))) for _ in range(60)]
+    allst = streams + small
+    rng.shuffle(allst)
+    src = bytearray()
+    hs = []
+    for i, st in enumerate(allst):
+        rec = O.record_set(b"fz%d" % i, 1 << 8 | 1, st, 4)
+        hs.append((len(src), len(rec), 0))
+        src += rec
+    h = np.array(hs, dtype=O.HANDLE_DT)
+    got, gvals, goff = codec.decode(bytes(src), h, compressor=1)
+    exp, evals, eoff = O.decode_batch(bytes(src), h, codec=1)
+    assert_desc_equal(got, exp)
+    assert np.array_equal(goff, eoff)
+    ok = np.nonzero(exp["status"] == 0)[0]
+    assert len(ok) >= len(small) + len(bases)
+    assert (exp["status"] == O.SNAPPY_CORRUPT).sum() >= 20
+    for i in ok:
+        assert gvals[int(goff[i]):int(goff[i + 1])].tobytes() == evals[int(eoff[i]):int(eoff[i + 1])].tobytes(), i
+
+
 def test_snappy_long_streams_in_lds(codec):
     """Streams longer than the 64 chunks a lane-per-chunk staging covers (1,025 .. 1,064 B
     for a <= 1 KiB value: values snappy cannot shrink) are decoded in their LDS slot, the
