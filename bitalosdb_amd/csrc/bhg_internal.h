@@ -59,9 +59,12 @@ hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, 
 // records: see long_batch)
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out, void *long_scratch = nullptr);
-// bhg_longcrc.hip: masked CRC-32C of the records longer than kLongRec, the whole chip at once (64-KiB
+// bhg_longcrc.hip: masked CRC-32C of the records longer than kLongRec, the whole chip at once (8-KiB
 // chunks, one workgroup each), completing descriptors the LONG tile kernel left (crc 0, status unchecked)
-constexpr uint32_t kLongRec = 16384;
+// (4 KiB: the tile kernel's 8 lanes per record load a record's windows past the first 9 one pass at
+// a time, synchronously; at 16 KiB the records of 4-16 KiB kept the bigval NoCompressor step's tile
+// kernel at 0.19 ms of 0.62)
+constexpr uint32_t kLongRec = 4096;
 // the dispatch's rule: the long-record pass runs for batches whose mean record is past this (the tile
 // kernel's own path stays for the rest: its rounds handle any length, a long record at 8 lanes)
 constexpr uint64_t kLongMean = 8192;

@@ -139,15 +139,16 @@ def np_bytes(g, n):
 @pytest.mark.parametrize("seed", [1, 2])
 def test_long_record_batches(codec, seed):
     """A NoCompressor batch whose mean record is past 8 KiB takes the long-record pass
-    (bhg_longcrc.hip): records over 16 KiB are CRC'd as 64-KiB chunks by the whole chip and the
+    (bhg_longcrc.hip): records over 4 KiB are CRC'd as 8-KiB pieces by the whole chip and the
     tile kernel leaves their CRC / status to it.  Mixed with short records, odd offsets, the
-    readRecord / readData statuses, lengths at the 16-KiB, 128-B and 64-KiB edges, 1-3 MiB
+    readRecord / readData statuses, lengths at the 4-KiB, 16-KiB, 128-B, 8-KiB and 64-KiB edges, 1-3 MiB
     records, and expected CRCs with some flipped."""
     rng = random.Random(seed)
     g = np.random.default_rng(seed)
     vlens = [g.integers(16400, 400000) for _ in range(150)] + [g.integers(1, 16000) for _ in range(30)]
     vlens += [(1 << 20) + int(g.integers(0, 2 << 20)) for _ in range(4)]
     vlens += [16384 - 60, 16384 - 59, 65536 - 60, 65536 - 59, 131072 - 52, 128 * 1000 - 52, 65536 * 3 + 1]
+    vlens += [4096 - 60, 4096 - 59, 4096 - 58, 8192 - 60, 8192 - 59, 8192 + 68, 12288 - 60]
     rng.shuffle(vlens)
     specs = [(rand_bytes(rng, rng.randrange(0, 48)), np_bytes(g, int(v)), rng.randrange(1 << 32)) for v in vlens]
     src, h = make_records(rng, specs, gap_max=3)
@@ -166,9 +167,9 @@ def test_long_record_batches(codec, seed):
 
 
 def test_long_record_pass_overflow_list(codec):
-    """Handles that overlap (the same 3-MiB record many times) give more chunks than the chunk
-    list holds (src_len / 64 KiB + n + 1): those records take the overflow walk, one workgroup
-    per record; the results must not depend on which path a record took."""
+    """Handles that overlap (the same 3-MiB record many times) give more pieces than the piece
+    list holds (src_len / 8 KiB + n + 1): those records take the overflow walk, one wave per
+    record; the results must not depend on which path a record took."""
     rng = random.Random(3)
     g = np.random.default_rng(3)
     src, h1 = make_records(rng, [(b"big-key", np_bytes(g, 3 << 20), 7), (b"small", b"v" * 100, 8)])
@@ -420,7 +421,7 @@ def test_snappy_segment_parse(codec, seed):
         hs.append((len(src), len(rec), 0))
         src += rec
     h = np.array(hs, dtype=O.HANDLE_DT)
-    # a batch of long records (mean past 8 KiB): the header pass leaves the records over 16 KiB to
+    # a batch of long records (mean past 8 KiB): the header pass leaves the records over 4 KiB to
     # the long-record CRC pass; expected CRCs with every 7th flipped check its status
     assert len(src) > 8192 * len(h)
     e0, _, _ = O.decode_batch(bytes(src), h, codec=1)
