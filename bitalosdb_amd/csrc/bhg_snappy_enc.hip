@@ -679,8 +679,9 @@ __global__ __launch_bounds__(64 * WPG, MINW) void k_snappy_enc(const uint8_t *__
     acc[5] = __builtin_amdgcn_s_memtime() - t_k0;
     if (lane == 0)
         for (int q = 0; q < 8; q++) atomicAdd((unsigned long long *)&se_prof[q], (unsigned long long)acc[q]);
-    if (gw == 0 && lane == 0)
-        printf("se_prof wave0: scan %llu lit %llu copy %llu phases %llu values %llu total %llu batches %llu duplanes %llu\n",
+    if ((gw & 255) == 0 && lane == 0)
+        printf("se_prof cap %d wave %u: scan %llu lit %llu copy %llu phases %llu values %llu total %llu batches %llu duplanes %llu\n",
+               CAP, gw,
                (unsigned long long)acc[0], (unsigned long long)acc[1], (unsigned long long)acc[2],
                (unsigned long long)acc[3], (unsigned long long)acc[4], (unsigned long long)acc[5],
                (unsigned long long)acc[6], (unsigned long long)acc[7]);
