@@ -194,3 +194,27 @@ def test_walk_rejects_what_the_restatement_rejects(walk, lanes):
         assert r in (1, 2), st
         walked += 1
     assert walked >= 4
+
+
+def test_walk_long_literal_length_bytes(walk, lanes):
+    """Literal lengths in 1-4 extra bytes (tags 60-63; golang/snappy writes 1-2 of them, any decoder
+    must take all four), including 4-byte lengths past the output (rejected), decode as the
+    restatement does."""
+    body = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    cases = []
+    for nb in (1, 2, 3, 4):
+        n = len(body)
+        cases.append(uvarint(n) + bytes([(59 + nb) << 2]) + (n - 1).to_bytes(nb, "little") + body)
+    cases.append(uvarint(8) + bytes([63 << 2]) + (0xFFFFFFFF).to_bytes(4, "little") + b"abcdefgh")
+    cases.append(uvarint(8) + bytes([63 << 2]) + (1 << 24).to_bytes(4, "little") + b"abcdefgh")
+    for st in cases:
+        try:
+            want = O.snappy_decode(st)
+        except O.SnappyCorrupt:
+            want = None
+        dl, _ = O.snappy_decoded_len(st)
+        r, out = run_slot(walk, st, dl, lanes=lanes)
+        if want is None:
+            assert r in (1, 2), st
+        else:
+            assert r == 0 and out == want, st
