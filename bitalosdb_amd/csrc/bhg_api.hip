@@ -1068,14 +1068,19 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
         blk_b = bhg::snappy_block_scratch_bytes(n, vals_len);
         cls_b = bhg::snappy_enc_list_bytes(n);
     }
+    // a batch of long values (mean past kLongMean, the decode's rule): records longer than kLongRec are
+    // copied and CRC'd by whole-chip passes (bhg_encode.hip k_enc_lcopy + bhg_longcrc.hip)
+    const size_t long_b = bhg::long_batch(vals_len, n) ? bhg::enc_long_scratch_bytes(n, out_cap) : 0;
     Scratch sc;
-    const size_t al6 = 6 * 256;
-    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + blk_b + cls_b + al6, sc)) return r;
+    const size_t al6 = 7 * 256;
+    if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + blk_b + cls_b + long_b + al6, sc))
+        return r;
     bhg::EncodeLaunch E;
     memset(&E, 0, sizeof E);
     E.lens = reinterpret_cast<uint64_t *>(sc.take(lens_b));
     uint64_t *vlen = reinterpret_cast<uint64_t *>(sc.take(vlen_b));
     E.scan_scratch = sc.take(scan_b);
+    E.long_scratch = long_b ? sc.take(long_b) : nullptr;
     if (codec == BHG_CODEC_SNAPPY) {
         uint8_t *snap = sc.take(snap_b);
         uint64_t *soff = reinterpret_cast<uint64_t *>(sc.take(soff_b));
@@ -1138,12 +1143,16 @@ int bhg_repack_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (n == 0) return encode_empty(c, o, L.stream);
     if (!src || !handles || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
     const size_t N = (size_t)n + 1;
+    // a compaction of long records: their copies and CRCs by whole-chip passes, as bhg_encode_batch's
+    const size_t long_b = bhg::long_batch(src_len, n) ? bhg::enc_long_scratch_bytes(n, out_cap) : 0;
     Scratch sc;
-    if (int r = scratch_alloc(c, L.stream, 7 * N * 8 + 3 * N * 4 + bhg::scan_scratch_bytes(n) + 12 * 256, sc)) return r;
+    if (int r = scratch_alloc(c, L.stream, 7 * N * 8 + 3 * N * 4 + bhg::scan_scratch_bytes(n) + long_b + 13 * 256, sc))
+        return r;
     bhg::EncodeLaunch E;
     memset(&E, 0, sizeof E);
     E.lens = reinterpret_cast<uint64_t *>(sc.take(N * 8));
     E.scan_scratch = sc.take(bhg::scan_scratch_bytes(n));
+    E.long_scratch = long_b ? sc.take(long_b) : nullptr;
     uint64_t *key_off = reinterpret_cast<uint64_t *>(sc.take(N * 8));
     uint32_t *key_len = reinterpret_cast<uint32_t *>(sc.take(N * 4));
     uint64_t *trailers = reinterpret_cast<uint64_t *>(sc.take(N * 8));

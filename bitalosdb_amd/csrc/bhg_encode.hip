@@ -47,6 +47,7 @@ struct EncArgs {
     uint64_t out_cap;
     uint64_t *lens;               // scratch: L per record, then exclusive scan -> positions (n+1)
     const uint32_t *xtab;         // the context's CrcR8 shift tables (bhg_crc_tables.h build_xtab)
+    uint32_t long_min;            // 0, or kLongRec: longer records are left to k_enc_lcopy + the long CRC pass
     bhg_encode_out o;
 };
 
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
         }
         if (ok && qa >= dend) a.o.crc[r] = crc_mask(~pc);  // the whole record was in the prefix dwords
         // ---------------- phase B: wave per record, the value from qa on
-        uint64_t todo = __ballot(ok && qa < dend);
+        uint64_t todo = __ballot(ok && qa < dend && !(a.long_min != 0 && L > a.long_min));
         while (todo) {
             int jr[2];
             jr[0] = __builtin_ctzll(todo);
@@ -536,6 +537,129 @@ hipError_t launch_repack_prep(const Launch &L, const uint8_t *src, uint64_t src_
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Long records (a batch of long values: bhg_encode_batch picks this by long_batch, as the decode
+// does).  k_enc_pack gives a record one wave, so a 1-4 MiB value was one wave's 16-B chunks plus a
+// Horner CRC while the rest of the GPU idled: k_enc_pack took 4.45 of the 25.3-ms bigval encode step
+// (bench.py --config bigval, profiles/r6/final/bigval_kernel_stats.csv).  Here k_enc_pack writes such
+// a record's prefix dwords only (phase A), then
+//   k_enc_lcount  lane per record: the 16-KiB output segments of its value part [qa, dend)
+//   (scan)        segment base per record
+//   k_enc_lemit   lane per record: its list entries {record, segment}
+//   k_enc_lcopy   wave per segment (persistent grid): the value bytes in 16-B output chunks from
+//                 20-B source windows, as phase B of k_enc_pack
+// and, once k_enc_meta has written each record's handle {P, L}, the decode's long-record CRC pass
+// (bhg_longcrc.hip) computes the masked CRC-32C of every record longer than kLongRec from the packed
+// output, the whole chip at once (crc(A || B) = Z_|B|(crc(A)) ^ crc_0(B) over 8-KiB pieces).
+constexpr uint32_t kEncSeg = 16384;  // output bytes per copy work item (16 chunks per lane)
+
+struct EncRec {  // a record's placement, as k_enc_pack computes it
+    uint64_t dst, dend, vdst, qa, vp, vend;
+    bool ok;
+};
+__device__ __forceinline__ EncRec enc_rec(const EncArgs &a, uint32_t i, uint32_t ntab) {
+    EncRec r;
+    const uint64_t P = a.lens[i];
+    const uint32_t L = (uint32_t)(a.lens[i + 1] - P);
+    r.ok = ntab != 0 && a.o.status[i] == BHG_ST_OK && fit_status(a, P, L) == BHG_ST_OK && L > a.long_min;
+    const uint32_t kl = key_len_of(a, i);
+    r.dst = (uint64_t)a.out + P;
+    r.dend = r.dst + L;
+    r.vdst = r.dst + 20 + kl;
+    r.qa = (r.vdst + 3) & ~3ull;
+    r.vp = (uint64_t)a.vals + a.vpos[i];
+    r.vend = r.vp + (uint32_t)a.vlen[i];
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_enc_lcount(EncArgs a, uint64_t *__restrict__ cnt) {
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+        const EncRec r = enc_rec(a, i, ntab);
+        cnt[i] = r.ok && r.qa < r.dend ? (r.dend - r.qa + kEncSeg - 1) / kEncSeg : 0ull;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_enc_lemit(const uint64_t *__restrict__ base, uint32_t n, uint2 *__restrict__ ent) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t b0 = base[i], b1 = base[i + 1];
+        for (uint64_t k = b0; k < b1; k++) ent[k] = make_uint2(i, (uint32_t)(k - b0));
+    }
+}
+
+#define ENC_LCOPY_WAVES 4
+__global__ __launch_bounds__(64 * ENC_LCOPY_WAVES) void k_enc_lcopy(EncArgs a, const uint64_t *__restrict__ base,
+                                                                  const uint2 *__restrict__ ent) {
+    const uint32_t ntab = (uint32_t)a.o.summary[1];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t total = base[a.n];
+    const uint64_t nw = (uint64_t)gridDim.x * ENC_LCOPY_WAVES, w0 = (uint64_t)blockIdx.x * ENC_LCOPY_WAVES + (threadIdx.x >> 6);
+    const uint64_t dummy = (uint64_t)a.lens;  // a valid, 16-B aligned address for loads whose result is unused
+    constexpr uint32_t K = kEncSeg / 1024;   // chunks per lane per segment
+    for (uint64_t g = w0; g < total; g += nw) {
+        const uint2 e = ent[g];
+        const EncRec r = enc_rec(a, e.x, ntab);
+        const uint64_t qs = r.qa + (uint64_t)kEncSeg * e.y;
+        const uint64_t qe = qs + kEncSeg < r.dend ? qs + kEncSeg : r.dend;
+        const uint32_t nc = (uint32_t)((qe - qs + 15) >> 4);
+        const uint64_t sb = r.vp + (qs - r.vdst);  // source of output byte qs
+        // a dword is loaded only if it holds a byte of the value, or lies inside the buffer the
+        // value is in (vals_end)
+        const uint64_t lim = a.vals_end > r.vend ? a.vals_end : ((r.vend + 3) & ~3ull);
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < K; k0 += 4) {
+            u32x4 wx[4];
+            uint32_t w4[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t c = lane + 64 * (k0 + k);
+                const uint64_t sa = (sb + 16ull * c) & ~3ull;
+                const bool use = c < nc;
+                wx[k] = gld<u32x4_a4>(use && sa + 16 <= lim ? sa : dummy);
+                w4[k] = gld<uint32_t>(use && sa + 20 <= lim ? sa + 16 : dummy);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t c = lane + 64 * (k0 + k);
+                if (c >= nc) continue;
+                const uint64_t s = sb + 16ull * c, sa = s & ~3ull;
+                uint32_t d[5] = {wx[k].x, wx[k].y, wx[k].z, wx[k].w, w4[k]};
+                if (sa + 20 > lim) {  // the value's last bytes at the end of its buffer: dword by dword
+#pragma unroll
+                    for (int z = 0; z < 5; z++) d[z] = sa + 4 * z < lim ? gld<uint32_t>(sa + 4 * z) : 0u;
+                }
+                const uint32_t f = (uint32_t)(s & 3);
+                const u32x4 y = {__builtin_amdgcn_alignbyte(d[1], d[0], f), __builtin_amdgcn_alignbyte(d[2], d[1], f),
+                                 __builtin_amdgcn_alignbyte(d[3], d[2], f), __builtin_amdgcn_alignbyte(d[4], d[3], f)};
+                const uint64_t q = qs + 16ull * c;
+                if (q + 16 <= r.dend) {
+                    gst<u32x4_a4>(q, y);
+                } else {  // the record's last chunk: whole dwords, then the bytes of a partial one
+                    const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                    for (int z = 0; z < 4; z++) {
+                        const uint64_t qz = q + 4 * z;
+                        if (qz + 4 <= r.dend) {
+                            gst<uint32_t>(qz, yy[z]);
+                        } else {
+#pragma unroll
+                            for (int b = 0; b < 4; b++)
+                                if (qz + b < r.dend) gst<uint8_t>(qz + b, (uint8_t)(yy[z] >> (8 * b)));
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+static size_t al256e(size_t x) { return (x + 255) & ~(size_t)255; }
+static uint64_t enc_seg_cap(uint32_t n, uint64_t out_cap) { return out_cap / kEncSeg + n + 1; }
+size_t enc_long_scratch_bytes(uint32_t n, uint64_t out_cap) {
+    return al256e(((size_t)n + 1) * 8) + al256e(scan_scratch_bytes(n)) + al256e((size_t)enc_seg_cap(n, out_cap) * 8) +
+           al256e((size_t)n * sizeof(bhg_handle)) + al256e(long_crc_scratch_bytes(n, out_cap));
+}
+
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     EncArgs a;
     a.keys = E.keys; a.key_off = E.key_off; a.trailers = E.trailers;
@@ -545,6 +669,7 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     a.single_table = E.single_table; a.max_tables = E.max_tables; a.init_size = E.init_size;
     a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
     a.xtab = L.xtab;
+    a.long_min = E.long_scratch ? kLongRec : 0u;
     const uint32_t g = lane_grid(L, E.n, 256);
     hipLaunchKernelGGL(k_enc_sizes, dim3(g), dim3(256), 0, L.stream, a);
     hipError_t e = launch_exclusive_scan_u64(L, E.lens, E.lens, E.n, E.scan_scratch);
@@ -556,7 +681,29 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     if (gp > capp) gp = capp;
     if (gp == 0) gp = 1;
     hipLaunchKernelGGL(k_enc_pack, dim3(gp), dim3(64 * ENC_WAVES), 0, L.stream, a);
-    hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, a);
+    if (!E.long_scratch) {
+        hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, a);
+    } else {
+        uint8_t *sp = static_cast<uint8_t *>(E.long_scratch);
+        uint64_t *base = reinterpret_cast<uint64_t *>(sp);
+        sp += al256e(((size_t)E.n + 1) * 8);
+        void *scan = sp;
+        sp += al256e(scan_scratch_bytes(E.n));
+        uint2 *ent = reinterpret_cast<uint2 *>(sp);
+        sp += al256e((size_t)enc_seg_cap(E.n, E.out_cap) * 8);
+        bhg_handle *rec = reinterpret_cast<bhg_handle *>(sp);
+        sp += al256e((size_t)E.n * sizeof(bhg_handle));
+        hipLaunchKernelGGL(k_enc_lcount, dim3(g), dim3(256), 0, L.stream, a, base);
+        if ((e = launch_exclusive_scan_u64(L, base, base, E.n, scan)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_enc_lemit, dim3(g), dim3(256), 0, L.stream, base, E.n, ent);
+        hipLaunchKernelGGL(k_enc_lcopy, dim3(L.num_cus * 8), dim3(64 * ENC_LCOPY_WAVES), 0, L.stream, a, base,
+                           (const uint2 *)ent);
+        // the records' handles {P, L} (the caller's o.rec when it asked for them), then their CRCs
+        EncArgs m = a;
+        if (!m.o.rec) m.o.rec = rec;
+        hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, m);
+        if ((e = launch_long_crc(L, E.out, E.out_cap, m.o.rec, E.n, nullptr, nullptr, sp, E.o.crc)) != hipSuccess) return e;
+    }
     if (E.o.table_size)
         hipLaunchKernelGGL(k_enc_tsize, dim3(lane_grid(L, E.max_tables, 256)), dim3(256), 0, L.stream, a);
     return hipGetLastError();

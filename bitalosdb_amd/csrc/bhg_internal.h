@@ -70,8 +70,9 @@ constexpr uint32_t kLongRec = 4096;
 constexpr uint64_t kLongMean = 8192;
 inline bool long_batch(uint64_t src_len, uint32_t n) { return n != 0 && src_len > (uint64_t)n * kLongMean; }
 size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len);
+// crc_out (the encoder): non-null -> crc_out[i] = the masked CRC of each long record i, descriptors untouched
 hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           const uint32_t *expected_crc, bhg_desc *out, void *scratch);
+                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out = nullptr);
 // bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
 // the shift tables it reads (Launch::stab) are built on the host once per context
 size_t stream_tab_words();
@@ -154,8 +155,12 @@ struct EncodeLaunch {
     uint64_t out_cap;
     uint64_t *lens;            // scratch n+1
     void *scan_scratch;
+    // nullable: enc_long_scratch_bytes(n, out_cap) bytes -> records longer than kLongRec are copied
+    // and CRC'd by whole-chip passes instead of one wave of k_enc_pack each (a batch of long values)
+    void *long_scratch;
     bhg_encode_out o;
 };
+size_t enc_long_scratch_bytes(uint32_t n, uint64_t out_cap);
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E);
 hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen);
 // bhg_repack_batch: AddIkey inputs parsed from stored records

@@ -55,10 +55,16 @@ __device__ __forceinline__ bool long_rec(const bhg_handle &h, uint64_t src_len) 
 __device__ __forceinline__ const uint32_t *zlong(const uint32_t *zl, uint32_t x) { return zl + 1024u * (x - kXLongLo); }
 
 // crc from the record's final state: the descriptor's crc, and its status against expected_crc
-// (the tile kernel checked every other field; RECORD_NIL records get their CRC too)
-__device__ __forceinline__ void lc_finish(bhg_desc *out, uint32_t i, uint32_t state, const uint32_t *expected_crc) {
-    uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
+// (the tile kernel checked every other field; RECORD_NIL records get their CRC too) -- or, for the
+// encoder (crc_out non-null), crc_out[i] alone
+__device__ __forceinline__ void lc_finish(bhg_desc *out, uint32_t *crc_out, uint32_t i, uint32_t state,
+                                          const uint32_t *expected_crc) {
     const uint32_t crc = crc_mask(~state);  // crc.go:31-33
+    if (crc_out != nullptr) {
+        crc_out[i] = crc;
+        return;
+    }
+    uint32_t *dw = reinterpret_cast<uint32_t *>(out + i);
     dw[8] = crc;
     if (dw[9] == BHG_ST_OK && expected_crc != nullptr && expected_crc[i] != crc) dw[9] = BHG_ST_CRC_MISMATCH;
 }
@@ -137,7 +143,8 @@ __global__ __launch_bounds__(256) void k_lc_emit(const uint8_t *__restrict__ src
 __global__ __launch_bounds__(kLcThreads) void k_lc_piece(const uint8_t *__restrict__ src, uint64_t src_len,
                                                         const bhg_handle *__restrict__ h, uint32_t n,
                                                         const uint32_t *__restrict__ expected_crc,
-                                                        bhg_desc *__restrict__ out, const uint64_t *__restrict__ base,
+                                                        bhg_desc *__restrict__ out, uint32_t *__restrict__ crc_out,
+                                                        const uint64_t *__restrict__ base,
                                                         uint64_t cap, const LcEnt *__restrict__ ent,
                                                         uint32_t *__restrict__ pst, const uint32_t *__restrict__ ovf,
                                                         const uint32_t *__restrict__ zl) {
@@ -230,20 +237,20 @@ __global__ __launch_bounds__(kLcThreads) void k_lc_piece(const uint8_t *__restri
             const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)piece_state(L, S), 63);
             s = k == 0 ? v : zap(Zt + 1024 * 6, s) ^ v;
         }
-        if (lane == 0) lc_finish(out, i, s, expected_crc);
+        if (lane == 0) lc_finish(out, crc_out, i, s, expected_crc);
     }
 }
 
 // lane per long record of the list: the XOR of its pieces' shifted states
 __global__ __launch_bounds__(256) void k_lc_fin(const uint64_t *__restrict__ base, uint32_t n, uint64_t cap,
                                                 const uint32_t *__restrict__ pst, const uint32_t *__restrict__ expected_crc,
-                                                bhg_desc *__restrict__ out) {
+                                                bhg_desc *__restrict__ out, uint32_t *__restrict__ crc_out) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t b0 = base[i], b1 = base[i + 1];
         if (b1 == b0 || b1 > cap) continue;  // not long, or walked by the overflow pass
         uint32_t s = 0;
         for (uint64_t k = b0; k < b1; k++) s ^= pst[k];
-        lc_finish(out, i, s, expected_crc);
+        lc_finish(out, crc_out, i, s, expected_crc);
     }
 }
 
@@ -257,7 +264,7 @@ size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len) {
 }
 
 hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           const uint32_t *expected_crc, bhg_desc *out, void *scratch) {
+                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out) {
     uint8_t *sp = static_cast<uint8_t *>(scratch);
     uint64_t *base = reinterpret_cast<uint64_t *>(sp);
     sp += al256(((size_t)n + 1) * 8);
@@ -276,8 +283,9 @@ hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len
     hipLaunchKernelGGL(k_lc_emit, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, src, h, base, n, cap, ent, ovf);
     // persistent: one workgroup per CU (the LDS tables), pieces wave-strided
     hipLaunchKernelGGL(k_lc_piece, dim3(L.num_cus), dim3(kLcThreads), 0, L.stream, src, src_len, h, n, expected_crc, out,
-                       base, cap, ent, pst, ovf, L.xtab + kXLong);
-    hipLaunchKernelGGL(k_lc_fin, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, base, n, cap, pst, expected_crc, out);
+                       crc_out, base, cap, ent, pst, ovf, L.xtab + kXLong);
+    hipLaunchKernelGGL(k_lc_fin, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, base, n, cap, pst, expected_crc, out,
+                       crc_out);
     return hipGetLastError();
 }
 

@@ -847,40 +847,91 @@ __global__ __launch_bounds__(64) void k_snappy_enc_blocks(const uint8_t *__restr
     }
 }
 
-// one wave per value of the block path: uvarint(len(src)) (encode.go Encode), then its blocks'
-// outputs in order, into the value's scratch range; clen[i] = the total
-__global__ __launch_bounds__(256) void k_snappy_concat(const uint64_t *__restrict__ val_off, uint32_t n,
-                                                       const uint64_t *__restrict__ bbase, const uint8_t *__restrict__ bscr,
-                                                       const uint64_t *__restrict__ bsoff,
-                                                       const uint32_t *__restrict__ bclen, uint8_t *__restrict__ scratch,
-                                                       uint64_t scap, const uint64_t *__restrict__ soff,
-                                                       uint64_t *__restrict__ clen) {
-    const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x / 64;
-    for (uint32_t i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+// one WAVE per block of the block path (persistent grid): the block's output copied to its place in
+// the value's scratch range -- after uvarint(len(src)) (encode.go Encode) and the outputs of the
+// value's earlier blocks, whose lengths the wave sums -- and, by block 0's wave, the header and
+// clen[i].  (A wave per VALUE copying 64 bytes per instruction took 1.54 ms of the bigval encode step
+// for the longest value's 2.3 MB, and 83 us of every C4 step launching a wave per value;
+// profiles/r6/final/.)
+#define SE_BCOPY_WAVES 4
+__global__ __launch_bounds__(64 * SE_BCOPY_WAVES) void k_snappy_bcopy(const uint64_t *__restrict__ val_off, uint32_t n,
+                                                                    const uint64_t *__restrict__ bbase,
+                                                                    const uint2 *__restrict__ ent,
+                                                                    const uint8_t *__restrict__ bscr,
+                                                                    const uint64_t *__restrict__ bsoff,
+                                                                    const uint32_t *__restrict__ bclen,
+                                                                    uint8_t *__restrict__ scratch, uint64_t scap,
+                                                                    const uint64_t *__restrict__ soff,
+                                                                    uint64_t *__restrict__ clen) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t total = bbase[n];
+    const uint64_t nw = (uint64_t)gridDim.x * SE_BCOPY_WAVES, w0 = (uint64_t)blockIdx.x * SE_BCOPY_WAVES + (threadIdx.x >> 6);
+    for (uint64_t q = w0; q < total; q += nw) {
+        const uint2 e = ent[q];
+        const uint32_t i = e.x, b = e.y;
         const uint64_t b0 = bbase[i], b1 = bbase[i + 1];
-        if (b0 == b1) continue;
         if (soff[i + 1] > scap) {  // val_off inconsistent with the vals_len the caller passed
-            if (lane == 0) clen[i] = ~0ull;
+            if (b == 0 && lane == 0) clen[i] = ~0ull;
             continue;
         }
-        uint8_t *d = scratch + soff[i];
-        uint64_t x = val_off[i + 1] - val_off[i];
-        uint32_t k = 0;
-        while (x >= 0x80) {
-            if (lane == 0) d[k] = (uint8_t)x | 0x80;
-            x >>= 7;
-            k++;
+        const uint64_t x = val_off[i + 1] - val_off[i];
+        uint32_t hdr = 1;
+        for (uint64_t y = x; y >= 0x80; y >>= 7) hdr++;
+        // the outputs before this block (all of them, for block 0's clen)
+        const uint32_t upto = b == 0 ? (uint32_t)(b1 - b0) : b;
+        uint64_t before = 0;
+        for (uint32_t k = lane; k < upto; k += 64) before += bclen[b0 + k];
+        for (int m = 1; m < 64; m <<= 1) before += (uint64_t)__shfl_xor((long long)before, m, 64);
+        uint8_t *d0 = scratch + soff[i];
+        if (b == 0) {
+            if (lane < hdr) d0[lane] = (uint8_t)((x >> (7 * lane)) & 0x7f) | (lane + 1 < hdr ? 0x80 : 0);
+            if (lane == 0) clen[i] = hdr + before;
+            before = 0;
         }
-        if (lane == 0) d[k] = (uint8_t)x;
-        uint64_t pos = k + 1;
-        const uint8_t *sb = bscr + bsoff[i];
-        for (uint64_t b = b0; b < b1; b++) {
-            const uint32_t len = bclen[b];
-            const uint8_t *s = sb + (b - b0) * kSeBlockMax;
-            for (uint32_t t = lane; t < len; t += 64) d[pos + t] = s[t];
-            pos += len;
+        const uint64_t dst = (uint64_t)d0 + hdr + before, len = bclen[q];
+        const uint64_t src = (uint64_t)bscr + bsoff[i] + (uint64_t)b * kSeBlockMax;
+        // bytes up to the first 4-aligned output address, then 16-B output chunks from 20-B source
+        // windows (the slot is MaxEncodedLen long, the buffer 64 B longer: the windows stay inside)
+        const uint64_t head = ((4u - (uint32_t)(dst & 3)) & 3u) < len ? ((4u - (uint32_t)(dst & 3)) & 3u) : len;
+        if (lane < head) reinterpret_cast<uint8_t *>(dst)[lane] = reinterpret_cast<const uint8_t *>(src)[lane];
+        const uint64_t qd = dst + head, qend = dst + len, sd = src + head;
+        const uint32_t nc = (uint32_t)((qend - qd + 15) >> 4);
+        for (uint32_t c0 = 0; c0 < nc; c0 += 256) {
+            u32x4 wx[4];
+            uint32_t w4[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t c = c0 + lane + 64 * k;
+                const uint64_t sa = (sd + 16ull * (c < nc ? c : 0u)) & ~3ull;
+                wx[k] = gld<u32x4_a4>(sa);
+                w4[k] = gld<uint32_t>(sa + 16);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t c = c0 + lane + 64 * k;
+                if (c >= nc) continue;
+                const uint32_t f = (uint32_t)((sd + 16ull * c) & 3);
+                const u32x4 y = {__builtin_amdgcn_alignbyte(wx[k].y, wx[k].x, f), __builtin_amdgcn_alignbyte(wx[k].z, wx[k].y, f),
+                                 __builtin_amdgcn_alignbyte(wx[k].w, wx[k].z, f), __builtin_amdgcn_alignbyte(w4[k], wx[k].w, f)};
+                const uint64_t o = qd + 16ull * c;
+                if (o + 16 <= qend) {
+                    gst<u32x4_a4>(o, y);
+                } else {
+                    const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                    for (int z = 0; z < 4; z++) {
+                        const uint64_t oz = o + 4 * z;
+                        if (oz + 4 <= qend) {
+                            gst<uint32_t>(oz, yy[z]);
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < 4; t++)
+                                if (oz + t < qend) gst<uint8_t>(oz + t, (uint8_t)(yy[z] >> (8 * t)));
+                        }
+                    }
+                }
+            }
         }
-        if (lane == 0) clen[i] = pos;
     }
 }
 
@@ -936,8 +987,8 @@ hipError_t launch_snappy_enc(const Launch &L, const uint8_t *vals, const uint64_
     hipLaunchKernelGGL(k_enc_bemit, dim3(lane_grid(L, n, 256)), dim3(256), 0, L.stream, bbase, n, ent);
     hipLaunchKernelGGL(k_snappy_enc_blocks, dim3(L.num_cus * kSeBlockWaves), dim3(64), 0, L.stream, vals, val_off, bbase,
                        n, ent, bhead, bscr, bsoff, bclen);
-    hipLaunchKernelGGL(k_snappy_concat, dim3(lane_grid(L, (uint64_t)n * 64, 256)), dim3(256), 0, L.stream, val_off, n,
-                       bbase, bscr, bsoff, bclen, scratch, scap, soff, clen);
+    hipLaunchKernelGGL(k_snappy_bcopy, dim3(L.num_cus * 8), dim3(64 * SE_BCOPY_WAVES), 0, L.stream, val_off, n, bbase,
+                       (const uint2 *)ent, bscr, bsoff, bclen, scratch, scap, soff, clen);
     return hipGetLastError();
 }
 

@@ -66,16 +66,20 @@ def test_k4_compact_iter_order(codec):
     assert np.array_equal(desc["fnv1"], np.array([O.fnv32(k) for k in keys], np.uint32))
 
 
-@pytest.mark.parametrize("compressor,init", [(0, 0), (1, 0), (0, 777)])
-def test_compaction_repack_pipeline(codec, compressor, init):
+@pytest.mark.parametrize("compressor,init,big", [(0, 0, False), (1, 0, False), (0, 777, False), (0, 0, True),
+                                                 (1, 0, True)])
+def test_compaction_repack_pipeline(codec, compressor, init, big):
+    """big: values of 3-120 KB, so the re-pack is a batch of long records (bhg_repack_batch's
+    long_batch rule): their value bytes copied by k_enc_lcopy and their CRCs by the long-record pass."""
     from bitalosdb_amd.codec import as_device_bytes
-    rng = random.Random(40 + compressor + init)
+    rng = random.Random(40 + compressor + init + 5 * big)
     st = T.Store(1 << 20, compressor=compressor)
     s = st.flush_start()
     live_keys = {}
-    for i in range(2500):
-        k = b"ck_%05d" % rng.randrange(1800)
-        s.add(k, i + 1, bytes(rng.randrange(65, 91) for _ in range(rng.choice([10, 300, 1500]))))
+    nadd, nkeys, sizes = (300, 200, [3000, 9000, 40000, 120000]) if big else (2500, 1800, [10, 300, 1500])
+    for i in range(nadd):
+        k = b"ck_%05d" % rng.randrange(nkeys)
+        s.add(k, i + 1, bytes(rng.randrange(65, 91) for _ in range(rng.choice(sizes))))
     s.compact = True
     s.finish()
     fns = sorted(st.files)

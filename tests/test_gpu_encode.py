@@ -78,6 +78,55 @@ def test_encode_long_keys_big_values(codec, compressor):
     check(got, exp)
 
 
+@pytest.mark.parametrize("compressor", [0, 1])
+def test_encode_long_batch(codec, compressor):
+    """A batch of long values (mean past 8 KiB): records longer than 4 KiB are left by k_enc_pack
+    to k_enc_lcopy (16-KiB output segments, one wave each) and their CRCs to the long-record pass over
+    the packed output.  Records of 4-5 KiB (one segment), values of several segments, user keys past
+    36 B, a long key with a 1-byte value (the whole value in the prefix dwords), a key too large and
+    short records in between; table splits at 1 MiB -- byte-exact with the restated writer, then
+    decoded back."""
+    rng = random.Random(70 + compressor)
+    g = np.random.default_rng(70 + compressor)
+    n = 120
+    keys, vals = [], []
+    for i in range(n):
+        kind = i % 6
+        klen = rng.choice([0, 1, 16, 32, 37, 64, 200])
+        if kind == 0:
+            v = rng.choice([4050, 4096, 4200, 5000, 16384 - 60, 16384 + 17])
+        elif kind == 1:
+            v = rng.choice([40000, 65536, 70001, 200000])
+        elif kind == 2:
+            v = rng.choice([1, 7, 300, 3000])
+        elif kind == 3:
+            v = rng.choice([100000, 333333])
+        elif kind == 4:
+            v = 1
+            klen = 5000  # L > 4 KiB from the key alone
+        else:
+            v = rng.choice([8192, 12000, 50000])
+        keys.append(rb(rng, klen))
+        vals.append(compressible(rng, v) if i % 2 else g.integers(0, 256, v, dtype=np.uint8).tobytes())
+    keys[11] = b"k" * ((33 << 10) - 7)  # KEY_TOO_LARGE
+    tr = [((i + 1) << 8) | 1 for i in range(n)]
+    got = codec.encode(keys, tr, vals, compressor=compressor, file_nums=list(range(1, 40)), table_max=1 << 20)
+    exp = O.encode_batch(keys, tr, vals, codec=compressor, file_nums=list(range(1, 40)), table_max=1 << 20)
+    assert sum(len(v) for v in vals) > 8192 * n  # a long batch (bhg_encode_batch's rule)
+    check(got, exp)
+    assert got["status"][11] == O.KEY_TOO_LARGE
+    h = np.zeros(n, dtype=O.HANDLE_DT)
+    h["offset"] = got["pos"]
+    h["length"] = got["bh_len"]
+    ok = np.nonzero(got["status"] == 0)[0]
+    desc, dv, doff = codec.decode(got["out"], h[ok], compressor=compressor)
+    assert (desc["status"] == 0).all()
+    assert (desc["crc"] == got["crc"][ok]).all()
+    for j, i in enumerate(ok):
+        if compressor:
+            assert dv[int(doff[j]):int(doff[j + 1])].tobytes() == vals[i]
+
+
 def test_encode_too_large(codec):
     rng = random.Random(8)
     keys = [b"a" * 10, b"b" * ((33 << 10) - 7), b"c" * 5, b"d" * ((33 << 10) - 8)]
@@ -160,7 +209,7 @@ def test_encode_snappy_byte_exact(codec, seed):
 @pytest.mark.parametrize("seed", [21, 22])
 def test_encode_snappy_block_path(codec, seed):
     """Values past 4 KiB: every 64-KiB block is a work item of its own (k_snappy_enc_blocks),
-    then each value's uvarint header and block outputs are joined (k_snappy_concat).  Sizes at
+    then each value's uvarint header and block outputs are joined (k_snappy_bcopy).  Sizes at
     the block edges (a last block of 16 bytes is emitLiteral'd, of 17 encodeBlock'd), 1-2 MiB
     values, incompressible / compressible / periodic / zero data, small values interleaved --
     byte-exact with the restated encoder, and decoded back on the GPU."""
