@@ -60,13 +60,15 @@ hipError_t launch_decode(const Launch &L, const uint8_t *src, uint64_t src_len, 
 hipError_t launch_decode_tile(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
                               const uint32_t *expected_crc, bhg_desc *out, void *long_scratch = nullptr);
 // bhg_longcrc.hip: masked CRC-32C of the records longer than kLongRec, the whole chip at once (8-KiB
-// chunks, one workgroup each), completing descriptors the LONG tile kernel left (crc 0, status unchecked)
+// pieces, one wave each), completing descriptors the LONG tile kernel left (crc 0, status unchecked),
+// or (the encoder) the CRCs of the long records k_enc_pack left to k_enc_lcopy
 // (4 KiB: the tile kernel's 8 lanes per record load a record's windows past the first 9 one pass at
 // a time, synchronously; at 16 KiB the records of 4-16 KiB kept the bigval NoCompressor step's tile
 // kernel at 0.19 ms of 0.62)
 constexpr uint32_t kLongRec = 4096;
-// the dispatch's rule: the long-record pass runs for batches whose mean record is past this (the tile
-// kernel's own path stays for the rest: its rounds handle any length, a long record at 8 lanes)
+// the dispatch's rule: the long-record passes run for batches whose mean record (decode) or value
+// (encode, repack) is past this (the tile kernel's and k_enc_pack's own paths stay for the rest: they
+// handle any length, a long record at one wave's or 8 lanes' pace)
 constexpr uint64_t kLongMean = 8192;
 inline bool long_batch(uint64_t src_len, uint32_t n) { return n != 0 && src_len > (uint64_t)n * kLongMean; }
 size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len);
