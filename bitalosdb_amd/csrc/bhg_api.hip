@@ -1070,7 +1070,8 @@ int bhg_encode_batch(bhg_ctx *c, const uint8_t *keys, const uint64_t *key_off, c
     }
     // a batch of long values (mean past kLongMean, the decode's rule): records longer than kLongRec are
     // copied and CRC'd by whole-chip passes (bhg_encode.hip k_enc_lcopy + bhg_longcrc.hip)
-    const size_t long_b = bhg::long_batch(vals_len, n) ? bhg::enc_long_scratch_bytes(n, out_cap) : 0;
+    const uint64_t vbound = codec == BHG_CODEC_SNAPPY ? snap_b : vals_len;  // the buffer value' bytes lie in
+    const size_t long_b = bhg::long_batch(vals_len, n) ? bhg::enc_long_scratch_bytes(n, vbound) : 0;
     Scratch sc;
     const size_t al6 = 7 * 256;
     if (int r = scratch_alloc(c, L.stream, lens_b + vlen_b + scan_b + snap_b + soff_b + blk_b + cls_b + long_b + al6, sc))
@@ -1144,7 +1145,7 @@ int bhg_repack_batch(bhg_ctx *c, const uint8_t *src, uint64_t src_len, const bhg
     if (!src || !handles || !out) { set_err(c, "null buffer"); return BHG_EINVAL; }
     const size_t N = (size_t)n + 1;
     // a compaction of long records: their copies and CRCs by whole-chip passes, as bhg_encode_batch's
-    const size_t long_b = bhg::long_batch(src_len, n) ? bhg::enc_long_scratch_bytes(n, out_cap) : 0;
+    const size_t long_b = bhg::long_batch(src_len, n) ? bhg::enc_long_scratch_bytes(n, src_len) : 0;
     Scratch sc;
     if (int r = scratch_alloc(c, L.stream, 7 * N * 8 + 3 * N * 4 + bhg::scan_scratch_bytes(n) + long_b + 13 * 256, sc))
         return r;

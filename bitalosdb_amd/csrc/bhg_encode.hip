@@ -48,6 +48,8 @@ struct EncArgs {
     uint64_t *lens;               // scratch: L per record, then exclusive scan -> positions (n+1)
     const uint32_t *xtab;         // the context's CrcR8 shift tables (bhg_crc_tables.h build_xtab)
     uint32_t long_min;            // 0, or kLongRec: longer records are left to k_enc_lcopy + the long CRC pass
+    const uint64_t *lbase;        // long mode: segment base per record (scanned k_enc_lcount), lbase[n] total
+    uint64_t lcap;                // long mode: segment list capacity (records past it stay with k_enc_pack)
     bhg_encode_out o;
 };
 
@@ -302,7 +304,9 @@ __global__ __launch_bounds__(64 * ENC_WAVES) void k_enc_pack(EncArgs a) {
         }
         if (ok && qa >= dend) a.o.crc[r] = crc_mask(~pc);  // the whole record was in the prefix dwords
         // ---------------- phase B: wave per record, the value from qa on
-        uint64_t todo = __ballot(ok && qa < dend && !(a.long_min != 0 && L > a.long_min));
+        // long mode: records whose segments k_enc_lemit listed are k_enc_lcopy's
+        const bool listed = a.lbase != nullptr && a.lbase[rr + 1] > a.lbase[rr] && a.lbase[rr + 1] <= a.lcap;
+        uint64_t todo = __ballot(ok && qa < dend && !listed);
         while (todo) {
             int jr[2];
             jr[0] = __builtin_ctzll(todo);
@@ -580,9 +584,16 @@ __global__ __launch_bounds__(256) void k_enc_lcount(EncArgs a, uint64_t *__restr
     }
 }
 
-__global__ __launch_bounds__(256) void k_enc_lemit(const uint64_t *__restrict__ base, uint32_t n, uint2 *__restrict__ ent) {
+// a record whose segments would pass the list's capacity is not listed (k_enc_pack keeps it: its
+// phase B copies it); later records then are not either (base is non-decreasing)
+__global__ __launch_bounds__(256) void k_enc_lemit(const uint64_t *__restrict__ base, uint32_t n, uint64_t cap,
+                                                   uint2 *__restrict__ ent) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t b0 = base[i], b1 = base[i + 1];
+        if (b1 > cap) {  // the list ends inside this record: its slots up to cap are marked empty
+            for (uint64_t k = b0; k < cap; k++) ent[k] = make_uint2(~0u, 0u);
+            continue;
+        }
         for (uint64_t k = b0; k < b1; k++) ent[k] = make_uint2(i, (uint32_t)(k - b0));
     }
 }
@@ -592,12 +603,13 @@ __global__ __launch_bounds__(64 * ENC_LCOPY_WAVES) void k_enc_lcopy(EncArgs a, c
                                                                   const uint2 *__restrict__ ent) {
     const uint32_t ntab = (uint32_t)a.o.summary[1];
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t total = base[a.n];
+    const uint64_t total = base[a.n] < a.lcap ? base[a.n] : a.lcap;
     const uint64_t nw = (uint64_t)gridDim.x * ENC_LCOPY_WAVES, w0 = (uint64_t)blockIdx.x * ENC_LCOPY_WAVES + (threadIdx.x >> 6);
     const uint64_t dummy = (uint64_t)a.lens;  // a valid, 16-B aligned address for loads whose result is unused
     constexpr uint32_t K = kEncSeg / 1024;   // chunks per lane per segment
     for (uint64_t g = w0; g < total; g += nw) {
         const uint2 e = ent[g];
+        if (e.x == ~0u) continue;  // an empty slot (the list ended inside a record)
         const EncRec r = enc_rec(a, e.x, ntab);
         const uint64_t qs = r.qa + (uint64_t)kEncSeg * e.y;
         const uint64_t qe = qs + kEncSeg < r.dend ? qs + kEncSeg : r.dend;
@@ -654,10 +666,16 @@ __global__ __launch_bounds__(64 * ENC_LCOPY_WAVES) void k_enc_lcopy(EncArgs a, c
 }
 
 static size_t al256e(size_t x) { return (x + 255) & ~(size_t)255; }
-static uint64_t enc_seg_cap(uint32_t n, uint64_t out_cap) { return out_cap / kEncSeg + n + 1; }
-size_t enc_long_scratch_bytes(uint32_t n, uint64_t out_cap) {
-    return al256e(((size_t)n + 1) * 8) + al256e(scan_scratch_bytes(n)) + al256e((size_t)enc_seg_cap(n, out_cap) * 8) +
-           al256e((size_t)n * sizeof(bhg_handle)) + al256e(long_crc_scratch_bytes(n, out_cap));
+// List capacities from the bytes the values lie in (vbound), not from out_cap (a caller may pass any
+// capacity): a record's value part is at most its value' bytes, and its header and key at most
+// 12 + 33 KiB + 8 (writer.go:42), so its 8-KiB CRC pieces number at most value'/8K + 6.  (A copy list
+// that overflowed would lose segments, so its bound must hold; the CRC pass walks records past its
+// list with one wave each.)
+static uint64_t enc_seg_cap(uint32_t n, uint64_t vbound) { return vbound / kEncSeg + n + 1; }
+static uint64_t enc_piece_cap(uint32_t n, uint64_t vbound) { return vbound / 8192 + 6ull * n + 1; }
+size_t enc_long_scratch_bytes(uint32_t n, uint64_t vbound) {
+    return al256e(((size_t)n + 1) * 8) + al256e(scan_scratch_bytes(n)) + al256e((size_t)enc_seg_cap(n, vbound) * 8) +
+           al256e((size_t)n * sizeof(bhg_handle)) + al256e(long_crc_scratch_bytes_cap(n, enc_piece_cap(n, vbound)));
 }
 
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
@@ -670,11 +688,36 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     a.table_max = E.table_max; a.out = E.out; a.out_cap = E.out_cap; a.lens = E.lens; a.o = E.o;
     a.xtab = L.xtab;
     a.long_min = E.long_scratch ? kLongRec : 0u;
+    a.lbase = nullptr;
+    a.lcap = 0;
     const uint32_t g = lane_grid(L, E.n, 256);
     hipLaunchKernelGGL(k_enc_sizes, dim3(g), dim3(256), 0, L.stream, a);
     hipError_t e = launch_exclusive_scan_u64(L, E.lens, E.lens, E.n, E.scan_scratch);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_enc_split, dim3(1), dim3(1024), 0, L.stream, a);
+    // long mode: the long records' copy segments listed before the pack, which leaves them alone
+    uint64_t *base = nullptr, vbound = 0;
+    uint2 *ent = nullptr;
+    bhg_handle *rec = nullptr;
+    uint8_t *crc_scratch = nullptr;
+    if (E.long_scratch) {
+        uint8_t *sp = static_cast<uint8_t *>(E.long_scratch);
+        vbound = (uint64_t)(E.vend - E.vbase);
+        base = reinterpret_cast<uint64_t *>(sp);
+        sp += al256e(((size_t)E.n + 1) * 8);
+        void *scan = sp;
+        sp += al256e(scan_scratch_bytes(E.n));
+        ent = reinterpret_cast<uint2 *>(sp);
+        sp += al256e((size_t)enc_seg_cap(E.n, vbound) * 8);
+        rec = reinterpret_cast<bhg_handle *>(sp);
+        sp += al256e((size_t)E.n * sizeof(bhg_handle));
+        crc_scratch = sp;
+        hipLaunchKernelGGL(k_enc_lcount, dim3(g), dim3(256), 0, L.stream, a, base);
+        if ((e = launch_exclusive_scan_u64(L, base, base, E.n, scan)) != hipSuccess) return e;
+        a.lbase = base;
+        a.lcap = enc_seg_cap(E.n, vbound);
+        hipLaunchKernelGGL(k_enc_lemit, dim3(g), dim3(256), 0, L.stream, (const uint64_t *)base, E.n, a.lcap, ent);
+    }
     uint32_t gp = (E.n + 64 * ENC_WAVES - 1) / (64 * ENC_WAVES);  // a wave per 64-record tile
     static const uint32_t per_cu = resident_per_cu((const void *)k_enc_pack, 64 * ENC_WAVES, 2);
     const uint32_t capp = (uint32_t)L.num_cus * per_cu;
@@ -684,25 +727,15 @@ hipError_t launch_encode(const Launch &L, const EncodeLaunch &E) {
     if (!E.long_scratch) {
         hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, a);
     } else {
-        uint8_t *sp = static_cast<uint8_t *>(E.long_scratch);
-        uint64_t *base = reinterpret_cast<uint64_t *>(sp);
-        sp += al256e(((size_t)E.n + 1) * 8);
-        void *scan = sp;
-        sp += al256e(scan_scratch_bytes(E.n));
-        uint2 *ent = reinterpret_cast<uint2 *>(sp);
-        sp += al256e((size_t)enc_seg_cap(E.n, E.out_cap) * 8);
-        bhg_handle *rec = reinterpret_cast<bhg_handle *>(sp);
-        sp += al256e((size_t)E.n * sizeof(bhg_handle));
-        hipLaunchKernelGGL(k_enc_lcount, dim3(g), dim3(256), 0, L.stream, a, base);
-        if ((e = launch_exclusive_scan_u64(L, base, base, E.n, scan)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_enc_lemit, dim3(g), dim3(256), 0, L.stream, base, E.n, ent);
-        hipLaunchKernelGGL(k_enc_lcopy, dim3(L.num_cus * 8), dim3(64 * ENC_LCOPY_WAVES), 0, L.stream, a, base,
-                           (const uint2 *)ent);
+        hipLaunchKernelGGL(k_enc_lcopy, dim3(L.num_cus * 8), dim3(64 * ENC_LCOPY_WAVES), 0, L.stream, a,
+                           (const uint64_t *)base, (const uint2 *)ent);
         // the records' handles {P, L} (the caller's o.rec when it asked for them), then their CRCs
         EncArgs m = a;
         if (!m.o.rec) m.o.rec = rec;
         hipLaunchKernelGGL(k_enc_meta, dim3(lane_grid(L, E.n, 256)), dim3(256), 0, L.stream, m);
-        if ((e = launch_long_crc(L, E.out, E.out_cap, m.o.rec, E.n, nullptr, nullptr, sp, E.o.crc)) != hipSuccess) return e;
+        if ((e = launch_long_crc(L, E.out, E.out_cap, m.o.rec, E.n, nullptr, nullptr, crc_scratch, E.o.crc,
+                                 enc_piece_cap(E.n, vbound))) != hipSuccess)
+            return e;
     }
     if (E.o.table_size)
         hipLaunchKernelGGL(k_enc_tsize, dim3(lane_grid(L, E.max_tables, 256)), dim3(256), 0, L.stream, a);

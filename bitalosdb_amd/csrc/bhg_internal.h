@@ -72,9 +72,13 @@ constexpr uint32_t kLongRec = 4096;
 constexpr uint64_t kLongMean = 8192;
 inline bool long_batch(uint64_t src_len, uint32_t n) { return n != 0 && src_len > (uint64_t)n * kLongMean; }
 size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len);
-// crc_out (the encoder): non-null -> crc_out[i] = the masked CRC of each long record i, descriptors untouched
+// the same for a piece list of cap entries (a record whose pieces pass it is walked by one wave instead)
+size_t long_crc_scratch_bytes_cap(uint32_t n, uint64_t cap);
+// crc_out (the encoder): non-null -> crc_out[i] = the masked CRC of each long record i, descriptors untouched;
+// list_cap: 0 (room for every piece of src_len) or the list capacity the scratch was sized for
 hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out = nullptr);
+                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out = nullptr,
+                           uint64_t list_cap = 0);
 // bhg_decode_stream.hip: mode 0 NoCompressor, mode 1 snappy header pass;
 // the shift tables it reads (Launch::stab) are built on the host once per context
 size_t stream_tab_words();
@@ -157,12 +161,13 @@ struct EncodeLaunch {
     uint64_t out_cap;
     uint64_t *lens;            // scratch n+1
     void *scan_scratch;
-    // nullable: enc_long_scratch_bytes(n, out_cap) bytes -> records longer than kLongRec are copied
+    // nullable: enc_long_scratch_bytes(n, vend - vbase) bytes -> records longer than kLongRec are copied
     // and CRC'd by whole-chip passes instead of one wave of k_enc_pack each (a batch of long values)
     void *long_scratch;
     bhg_encode_out o;
 };
-size_t enc_long_scratch_bytes(uint32_t n, uint64_t out_cap);
+// vbound: the bytes of the buffer the values' (value') bytes lie in (EncodeLaunch vend - vbase)
+size_t enc_long_scratch_bytes(uint32_t n, uint64_t vbound);
 hipError_t launch_encode(const Launch &L, const EncodeLaunch &E);
 hipError_t launch_enc_rawvals(const Launch &L, const uint64_t *val_off, uint32_t n, uint64_t *vlen);
 // bhg_repack_batch: AddIkey inputs parsed from stored records

@@ -257,20 +257,21 @@ __global__ __launch_bounds__(256) void k_lc_fin(const uint64_t *__restrict__ bas
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 static uint64_t lc_cap(uint32_t n, uint64_t src_len) { return src_len / kLcPiece + n + 1; }
 
-size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len) {
-    const uint64_t cap = lc_cap(n, src_len);
+size_t long_crc_scratch_bytes_cap(uint32_t n, uint64_t cap) {
     return al256(((size_t)n + 1) * 8) + al256(scan_scratch_bytes(n)) + al256((size_t)cap * sizeof(LcEnt)) +
            al256((size_t)cap * 4) + al256(((size_t)n + 1) * 4);
 }
+size_t long_crc_scratch_bytes(uint32_t n, uint64_t src_len) { return long_crc_scratch_bytes_cap(n, lc_cap(n, src_len)); }
 
 hipError_t launch_long_crc(const Launch &L, const uint8_t *src, uint64_t src_len, const bhg_handle *h, uint32_t n,
-                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out) {
+                           const uint32_t *expected_crc, bhg_desc *out, void *scratch, uint32_t *crc_out,
+                           uint64_t list_cap) {
     uint8_t *sp = static_cast<uint8_t *>(scratch);
     uint64_t *base = reinterpret_cast<uint64_t *>(sp);
     sp += al256(((size_t)n + 1) * 8);
     void *scan = sp;
     sp += al256(scan_scratch_bytes(n));
-    const uint64_t cap = lc_cap(n, src_len);
+    const uint64_t cap = list_cap ? list_cap : lc_cap(n, src_len);
     LcEnt *ent = reinterpret_cast<LcEnt *>(sp);
     sp += al256((size_t)cap * sizeof(LcEnt));
     uint32_t *pst = reinterpret_cast<uint32_t *>(sp);

@@ -175,3 +175,34 @@ def test_repack_short_ikey(codec):
     size = int(bufs.table_size[0].item())
     assert out_t[:size].cpu().numpy().tobytes() == bytes(w.file)
     assert bytes(w.file).count(struct.pack("<III", 8, 9, 6) + struct.pack("<Q", 255) + b"012345678") == 1
+
+
+def test_repack_long_records_repeated(codec):
+    """A re-pack of long records (a long batch) whose handles name each record of the source
+    several times: the value bytes to copy then pass the source's size, which the copy list is
+    sized for, so the records past the list stay with k_enc_pack's own copy (its phase B) -- the
+    output is the records, in handle order, byte for byte, whichever pass copied them; every
+    record's CRC matches the restated writer's."""
+    from bitalosdb_amd.codec import as_device_bytes, handles_tensor
+    rng = np.random.default_rng(77)
+    sizes = [5000, 20000, 70000, 150000, 9000, 40000]
+    recs = [O.record_set(b"lkey%d" % i, (i + 1) << 8 | 1, rng.integers(0, 256, sizes[i], dtype=np.uint8).tobytes(), 3)
+            for i in range(len(sizes))]
+    src = b"".join(recs)
+    offs = np.cumsum([0] + [len(r) for r in recs])
+    order = [i % len(recs) for i in range(5 * len(recs))]  # every record 5 times
+    h = np.array([(int(offs[i]), len(recs[i]), 0) for i in order], dtype=O.HANDLE_DT)
+    want = b"".join(recs[i] for i in order)
+    assert len(src) > 8192 * len(order)  # a long batch by bhg_repack_batch's rule (mean past 8 KiB)
+    with torch.cuda.stream(codec.stream):
+        src_t = as_device_bytes(src, codec.device)
+        ht = handles_tensor(h, codec.device)
+        out_t = torch.zeros(len(want) + 64, dtype=torch.uint8, device=codec.device)
+        out_t, bufs = codec.repack_batch(src_t, ht, len(order), out_t=out_t)
+        codec.sync()
+    st = bufs.status.cpu().numpy().view(np.uint32)
+    assert (st == 0).all()
+    size = int(bufs.table_size[0].item())
+    assert out_t[:size].cpu().numpy().tobytes() == want
+    crc = bufs.crc.cpu().numpy().view(np.uint32)
+    assert list(crc) == [O.crc_masked(recs[i]) for i in order]
