@@ -108,6 +108,7 @@ constexpr uint32_t kSnapBucketBytes = 3072 / kSnapBuckets;  // decoded bytes per
 constexpr uint32_t kSnapSubs = 64 * (1 + kSnapBuckets);
 constexpr uint32_t kSnapRtCount = kSnapSubs;  // word of the global-memory list's size
 constexpr uint32_t kSnapListHdr = (kSnapSubs + 1 + 255) / 256 * 256;  // the sizes, rounded to 1 KiB
+constexpr uint32_t kSnapBigCtr = 384;  // 4 words of the header for launch_snappy's big-block path (zeroed with it)
 constexpr uint32_t kSnapSmallMax = 1024;   // decoded bytes a tier-1 slot takes ...
 constexpr uint32_t kSnapSmallSlot = 1088;  // ... and its slot (the stream + 24 must fit too)
 inline size_t snappy_sub_cap(uint32_t n) { return 64 * (((size_t)n + 64 * 64 - 1) / (64 * 64)); }

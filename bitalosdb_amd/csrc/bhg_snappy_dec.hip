@@ -1330,8 +1330,13 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         }
         // then the blocks the tiers handed on (too big for a slot, or an in-place spill): chunk-parallel
         // (k_sb_parse, k_sb_walk), and lane per block from global memory for the ones that need it
-        const SbScratch B = sb_layout(big, n, out_cap);
-        if (hipError_t e = hipMemsetAsync(B.ctr, 0, 16, L.stream)) return e;
+        const SbScratch B0 = sb_layout(big, n, out_cap);
+        // the big path's 4 counters live in the list header, which launch_decode zeroes before the
+        // header pass: one memset launch fewer per decode (C3 paid ~3 us for it)
+        static_assert(kSnapRtCount + 1 <= kSnapBigCtr && kSnapBigCtr + 4 <= kSnapListHdr && kSnapBigCtr % 4 == 0,
+                      "counters in the zeroed list header");
+        SbScratch B = B0;
+        B.ctr = list + kSnapBigCtr;
         hipLaunchKernelGGL(k_sb_parse, dim3(L.num_cus * 4), dim3(256), 0, L.stream, src, src_len, h, n, out, out_cap,
                            val_off, (const uint32_t *)c_rt, (const uint32_t *)e_rt, B.ctr, B.ent, B.cap, B.blk, B.ser,
                            B.bigs, B.segblk, B.segcap);
