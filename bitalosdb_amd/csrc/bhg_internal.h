@@ -101,7 +101,7 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
                          bhg_desc *out, uint8_t *out_vals, uint64_t out_cap, const uint64_t *val_off,
                          uint32_t *list, void *big);
 size_t snappy_big_bytes(uint32_t n, uint64_t out_cap);
-// size buckets of the 4-KiB tier, so a wave's 6 blocks walk alike (it runs as long as its longest):
+// size buckets of the 4-KiB tier, so a wave's blocks walk alike (it runs as long as its longest):
 // mixdec 4.89 -> 4.28 ms with 4; 8 and 12 buckets 4.31-4.32 / 4.36-4.39 (profiles/r5/snappy_buckets)
 constexpr uint32_t kSnapBuckets = 4;
 constexpr uint32_t kSnapBucketBytes = 3072 / kSnapBuckets;  // decoded bytes per bucket above 1 KiB

@@ -497,8 +497,8 @@ __device__ __forceinline__ uint32_t snappy_walk_lds(uint8_t *lds, uint32_t sp, u
 // entries apart): <= 1 KiB decoded with the stream fitting 1,088 B (tier 1), and 4 buckets of
 // decoded size above it (tier 2).  k_snappy_lds_nat walks the batch in its own order when >= 7/8
 // of it is small (C3); k_snappy_lds_multi runs every list in one launch, largest slots first: the
-// buckets in 4,160 / 3,392 / 2,624 / 1,856-B slots (6 / 7 / 9 / 13 blocks per wave), then tier 1's
-// list (23 per wave) unless the batch went in its own order.  What neither holds (over 4 KiB, an
+// buckets in 4,160 / 3,392 / 2,624 / 1,856-B slots (4 / 5 / 7 / 10 blocks per wave), then tier 1's
+// list (18 per wave) unless the batch went in its own order.  What neither holds (over 4 KiB, an
 // in-place spill) goes to k_snappy_rt (out_cnt / out_ent).
 // Measured on the C4-shaped decode (bench.py --config mixdec: 1M values U[64, 4096], 76 % of
 // them > 1 KiB; profiles/r5/snappy_*): the > 1 KiB blocks took 5.83 ms per step in k_snappy_rt
@@ -740,7 +740,10 @@ __global__ __launch_bounds__(64) void k_snappy_lds_nat(const uint8_t *__restrict
 // slots sized to it, then tier 1's list (unless tier 1 ran in batch order).  One launch, so the
 // empty roles of an all-1-KiB batch cost one start-up, and a role's tail overlaps the next one's
 // groups.
-constexpr uint32_t kMultiLds = 23 * 1088 + 64;  // the largest role (6 x 4,160 + 64 = 25,024 B is next)
+// The role shapes are sized for 8 one-wave workgroups per CU (2 waves per SIMD): 19.2 KiB of LDS each.
+// The round-5 shapes (6 / 7 / 9 / 13 / 23 blocks, 24.5 KiB) left 6 waves per CU, 2-2-1-1 over the
+// SIMDs: mixdec 288.8-289.4 -> 305.6-306.7 GiB/s (3 alternating runs, profiles/r6/lab_r6b/ item 9).
+constexpr uint32_t kMultiLds = 18 * 1088 + 64;  // the largest role (10 x 1,856 + 64 = 18,624 B is next)
 template <int G1, int G2>
 __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restrict__ src, uint64_t src_len,
                                                          const bhg_handle *__restrict__ handles, uint32_t n,
@@ -749,22 +752,22 @@ __global__ __launch_bounds__(64) void k_snappy_lds_multi(const uint8_t *__restri
                                                          uint32_t *__restrict__ list, uint32_t sub_cap) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kMultiLds];
     static_assert(kSnapBuckets == 4 && kSnapBucketBytes == 768, "the bucket slot sizes below");
-    static_assert(6 * 4160 + 64 <= kMultiLds && 7 * 3392 + 64 <= kMultiLds && 9 * 2624 + 64 <= kMultiLds && 13 * 1856 + 64 <= kMultiLds &&
-                      23 * 1088 + 64 <= kMultiLds, "roles fit the LDS");
+    static_assert(4 * 4160 + 64 <= kMultiLds && 5 * 3392 + 64 <= kMultiLds && 7 * 2624 + 64 <= kMultiLds && 10 * 1856 + 64 <= kMultiLds &&
+                      18 * 1088 + 64 <= kMultiLds, "roles fit the LDS");
     const uint32_t *c_small = list, *c_large = list + 64;
     uint32_t *c_rt = list + kSnapRtCount;
     const uint32_t *e_small = list + kSnapListHdr, *e_large = e_small + (size_t)64 * sub_cap;
     uint32_t *e_rt = list + kSnapListHdr + (size_t)kSnapSubs * sub_cap;
     const size_t bs = (size_t)64 * sub_cap;
-    sl_role<6, 4160, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large, e_large, sub_cap,
+    sl_role<4, 4160, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large, e_large, sub_cap,
                                c_rt, e_rt);
-    sl_role<7, 3392, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 64,
+    sl_role<5, 3392, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 64,
                                e_large + bs, sub_cap, c_rt, e_rt);
-    sl_role<9, 2624, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 128,
+    sl_role<7, 2624, 2, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 128,
                                e_large + 2 * bs, sub_cap, c_rt, e_rt);
-    sl_role<13, 1856, 1, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 192,
+    sl_role<10, 1856, 1, 0, 64, G2>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_large + 192,
                                 e_large + 3 * bs, sub_cap, c_rt, e_rt);
-    sl_role<23, 1088, 1, 1, 64, G1>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
+    sl_role<18, 1088, 1, 1, 64, G1>(lds, src, src_len, handles, n, out, out_vals, out_cap, val_off, c_small, e_small,
                                 sub_cap, c_rt, e_rt);
 }
 
@@ -1322,7 +1325,7 @@ hipError_t launch_snappy(const Launch &L, const uint8_t *src, uint64_t src_len, 
         {
             static const uint32_t per_cu =
                 resident_per_cu((const void *)k_snappy_lds_multi<kG1, kG2>, 64, (160u * 1024u) / kMultiLds);
-            const uint32_t groups = (n + 5) / 6, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
+            const uint32_t groups = (n + 3) / 4, lim = (uint32_t)L.num_cus * (per_cu ? per_cu : 1u);
             const uint32_t grid = groups < lim ? (groups ? groups : 1u) : lim;
             hipLaunchKernelGGL((k_snappy_lds_multi<kG1, kG2>), dim3(grid), dim3(64), 0, L.stream, src, src_len, h, n, out,
                                out_vals, out_cap, val_off, list, cap);
